@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""BMFR frame throughput on MI355X.
+
+One step = one frame of the BMFR hot path (bmfr.cpp:417-485: accumulate_noisy
+-> fitter -> weighted_sum -> accumulate_filtered -> taa), run by libbmfr's
+fused kernels (K1 per 32x32 block + K2 TAA) on synthetic 1-spp frames that
+are rendered on the GPU and resident in HBM before timing starts (the
+reference also excludes uploads and readback, bmfr.cpp:415-416,478).
+
+Workload at N=1: 3840x2160, reference default parameters (B = 13 features,
+half tmp_data, 32x32 blocks), frames W..W+K-1 of the sequence (temporal path
+active on every timed frame).
+
+Multi-GPU (torchrun, one process per GPU): weak scaling, each rank
+denoises its own 3840x2160 sequence; no data-path collective (see DESIGN.md
+"Multi-GPU").  Timing: barrier + synchronize around K frames, max over ranks.
+
+Extra JSON fields: `roofline` for the dominant kernel (K1), measured with HIP
+events on the stream it runs on; `cpu_baseline` = the CPU oracle
+(oracle/liboracle.so, OpenMP) on a bounded sample of the same sequence.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import bmfr_amd  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# Algorithmic bytes per pixel (SURVEY.md §8d, 18*s + 74 with s = 4 for f32 planes):
+#   K1 reads noisy/normal/position/albedo (48) + previous normal/position (24)
+#   + accumulated noisy (12) + spp (1) + accumulated filtered (12) and writes
+#   accumulated noisy (12) + spp (1) + accumulated filtered (12) = 122;
+#   K2 reads the previous TAA output (12) and writes the output (12) = 24.
+K1_BYTES_PER_PX = 122
+FRAME_BYTES_PER_PX = 146
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--half-tmp", type=int, default=1)
+    ap.add_argument("--third-order", action="store_true", help="B = 16 feature set (BASELINE config 5)")
+    ap.add_argument("--cpu-frames", type=int, default=2, help="timed CPU-oracle frames (0 = skip)")
+    ap.add_argument("--seed", type=int, default=0x424D4652)
+    return ap.parse_args()
+
+
+def psnr(a: np.ndarray, b: np.ndarray) -> float:
+    mse = float(np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2))
+    return 10 * np.log10(1.0 / mse) if mse > 0 else float("inf")
+
+
+def cpu_baseline(cfg: bmfr_amd.BmfrConfig, frames: int, seed: int):
+    """CPU oracle on the first frames+1 frames of the same sequence; frame 0
+    untimed (the reference's Total also starts at frame 1, bmfr.cpp:497-502)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    W, H = cfg.image_width, cfg.image_height
+    loop = pyoracle.OracleLoop(pyoracle.make_cfg(W, H, cfg.not_scaled, cfg.scaled,
+                                                 cfg.use_half_precision_in_tmp_data))
+    times = []
+    for f in range(frames + 1):
+        fr = bmfr_amd.synth_frame_host(W, H, f, seed=seed)
+        vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+        _, jit = bmfr_amd.synth_camera(W, H, f)
+        loop.upload(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"])
+        t0 = time.perf_counter()
+        loop.run_stages(vp, jit, f)
+        dt = time.perf_counter() - t0
+        loop.swap()
+        if f > 0:
+            times.append(dt)
+    ms = 1e3 * float(np.mean(times))
+    return {"value": round(ms, 2), "unit": "ms/frame", "cores": pyoracle.load().oracle_threads(),
+            "kind": "port",
+            "sample": f"{W}x{H} frames 1..{frames} of the same synthetic sequence (frame 0 untimed), "
+                      f"oracle/bmfr_oracle.c with OpenMP"}
+
+
+def pmc_traffic(workload: str):
+    """HBM bytes per K1 launch from the committed rocprofv3 PMC summary
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), when one exists for this workload."""
+    p = os.path.join(ROOT, "profiles", "pmc_k1.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    return d.get(workload, {}).get("hbm_bytes_per_launch")
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    W, H = a.width, a.height
+    scaled = bmfr_amd.SCALED_THIRD_ORDER if a.third_order else bmfr_amd.SCALED_DEFAULT
+    cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, scaled=scaled,
+                              use_half_precision_in_tmp_data=a.half_tmp)
+    den = bmfr_amd.Denoiser(cfg, device=local)
+    nfr = a.warmup + a.steps
+    seed = a.seed + rank  # each rank its own sequence (weak scaling)
+
+    # Render every frame into HBM up front (untimed).
+    frames = [bmfr_amd.synth_frame_device(W, H, f, seed=seed, device=local) for f in range(nfr)]
+    cams = []
+    for f in range(nfr):
+        vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+        _, jit = bmfr_amd.synth_camera(W, H, f)
+        cams.append((vp, jit))
+    torch.cuda.synchronize()
+
+    def run(f):
+        fr = frames[f]
+        prev = frames[f - 1] if f > 0 else None
+        den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], cams[f][0], cams[f][1], f,
+                          prev_normals=prev["normals"] if prev else None,
+                          prev_positions=prev["positions"] if prev else None)
+
+    for f in range(a.warmup):
+        run(f)
+    torch.cuda.synchronize()
+    den.set_profiling(True, capacity=max(a.steps, 1))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for f in range(a.warmup, nfr):
+        run(f)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = den.profile()
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_frame = 1e3 * elapsed / a.steps
+    k1_ms = float(np.mean([p[1] for p in prof]))
+    k2_ms = float(np.mean([p[2] for p in prof]))
+    dev_ms = float(np.mean([p[3] for p in prof]))
+    px = W * H
+    workload = f"bmfr_{W}x{H}_B{cfg.buffer_count}_{'half' if a.half_tmp else 'f32'}tmp"
+
+    # Quality: PSNR of the last output against the clean render of that frame.
+    clean = bmfr_amd.synth_frame_device(W, H, nfr - 1, seed=seed, device=local, clean=True)["clean"]
+    out = den.copy_output(torch.empty(px * 3, device="cuda"))
+    torch.cuda.synchronize()
+    q = psnr(out.cpu().numpy(), clean.cpu().numpy())
+    noisy_tm = torch.clamp(torch.clamp(frames[nfr - 1]["albedo"] * frames[nfr - 1]["noisy"], min=0) ** 0.454545,
+                           0, 1)
+    q_in = psnr(noisy_tm.cpu().numpy(), clean.cpu().numpy())
+
+    if rank == 0:
+        achieved = K1_BYTES_PER_PX * px / (k1_ms * 1e-3) / 1e9
+        line = {
+            "metric": "ms/frame @1080p & 4K, 1/2/4/8 GPU; PSNR vs 4096spp reference",
+            "value": round(ms_per_frame, 4),
+            "unit": "ms/frame",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_frame, 4),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" + ("+f16 tmp_data" if a.half_tmp else ""),
+            "data": "synthetic (GPU-rendered 1-spp frames + features, resident in HBM)",
+            "config": {"workload": workload, "image": f"{W}x{H}", "buffer_count": cfg.buffer_count,
+                       "half_tmp_data": a.half_tmp, "frames_timed": a.steps,
+                       "parallelism": f"replica x{world}" if world > 1 else "single GPU"},
+            "device_ms_per_frame": round(dev_ms, 4),
+            "kernel_ms": {"fused_block_k1": round(k1_ms, 4), "taa_k2": round(k2_ms, 4)},
+            "psnr_db": {"output": round(q, 2), "noisy_input": round(q_in, 2)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(workload),
+                         "kernel": "k_fused_block (K1)",
+                         "algorithmic_bytes_per_launch": K1_BYTES_PER_PX * px,
+                         "frame_frac": round(FRAME_BYTES_PER_PX * px / (ms_per_frame * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                             4)},
+        }
+        if world == 1 and a.cpu_frames > 0:
+            line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_frames, seed)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

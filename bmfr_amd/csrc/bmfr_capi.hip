@@ -1,0 +1,408 @@
+// bmfr_capi.hip -- implementation of include/bmfr.h.
+//
+// Replaces the reference's host plumbing around the hot path: CLEnv context /
+// queue / program creation (bmfr.cpp:183-243), buffer creation
+// (bmfr.cpp:315-347), kernel argument binding (bmfr.cpp:349-383, 429-476) and
+// the Double_buffer swap (bmfr.cpp:122-135, 482-484).  No allocation happens
+// on the per-frame path; every call returns a status code.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "../../include/bmfr.h"
+#include "bmfr_launch.h"
+
+using bmfr::Params;
+
+struct bmfr_ctx {
+    bmfr_config cfg;
+    bmfr_sizes sizes;
+    Params P;
+    int device;
+    // Temporal state, double-buffered (index `cur` is this frame's).
+    float* noisy_acc[2] = {nullptr, nullptr};
+    uint8_t* spp[2] = {nullptr, nullptr};
+    float* acc[2] = {nullptr, nullptr};
+    float* result[2] = {nullptr, nullptr};
+    float* tone = nullptr;
+    float2* prev_pixel = nullptr;
+    int cur = 0;
+    bool has_frame = false;
+    // Profiling ring: 3 events per frame (before K1, after K1, after K2).
+    int prof_capacity = 0;
+    long prof_count = 0;
+    hipEvent_t* prof_events = nullptr;
+    int* prof_frames = nullptr;
+};
+
+namespace {
+
+thread_local int g_last_hip_error = 0;
+
+bmfr_status hip_status(hipError_t e) {
+    if (e == hipSuccess) return BMFR_OK;
+    g_last_hip_error = (int)e;
+    if (e == hipErrorOutOfMemory) return BMFR_ERROR_OUT_OF_MEMORY;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return BMFR_ERROR_NO_DEVICE;
+    return BMFR_ERROR_HIP;
+}
+
+// `operator<<` of a double with default stream flags == printf("%g"); the
+// kernel then sees convert_float(<that text>) (bmfr.cpp:226-227, bmfr.cl:393).
+float as_kernel_literal(double v) {
+    char buf[64];
+    std::snprintf(buf, sizeof buf, "%g", v);
+    return (float)std::strtod(buf, nullptr);
+}
+
+bmfr_status validate(const bmfr_config* c) {
+    if (!c) return BMFR_ERROR_INVALID_ARGUMENT;
+    // mirror() is only valid less than one image size out of range
+    // (bmfr.cl:207-216).  Margin work-items reach pixel -32 and WORKSET+29
+    // (gid - 16 + BLOCK_OFFSETS, bmfr.cl:314-315), so both need
+    // -size <= p <= 2*size-1; smaller images read out of bounds upstream.
+    for (int d = 0; d < 2; ++d) {
+        const int n = d ? c->image_height : c->image_width;
+        const int E = BMFR_BLOCK_EDGE_LENGTH;
+        const int workset = E * ((n + E - 1) / E);
+        if (n < E || workset + 30 > 2 * n) return BMFR_ERROR_INVALID_ARGUMENT;
+    }
+    if (c->features_not_scaled < 0 || c->features_scaled < 0 ||
+        c->features_not_scaled + c->features_scaled > BMFR_MAX_FEATURES ||
+        c->features_not_scaled + c->features_scaled < 1)
+        return BMFR_ERROR_INVALID_ARGUMENT;
+    for (int i = 0; i < c->features_not_scaled + c->features_scaled; ++i)
+        if (c->feature_buffers[i] < 0 || c->feature_buffers[i] >= BMFR_FEATURE_COUNT_)
+            return BMFR_ERROR_INVALID_ARGUMENT;
+    if (c->tile_x || c->tile_y || c->tile_width || c->tile_height) return BMFR_ERROR_UNSUPPORTED;
+    return BMFR_OK;
+}
+
+Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
+    Params P{};
+    P.width = c->image_width;
+    P.height = c->image_height;
+    P.workset_w = s->workset_width;
+    P.workset_h = s->workset_height;
+    P.margins_w = s->workset_with_margins_width;
+    P.margins_h = s->workset_with_margins_height;
+    P.blocks_x = P.margins_w / BMFR_BLOCK_EDGE_LENGTH;
+    P.blocks_y = P.margins_h / BMFR_BLOCK_EDGE_LENGTH;
+    P.buffers = s->buffer_count;
+    P.not_scaled = c->features_not_scaled;
+    P.scaled = c->features_scaled;
+    for (int i = 0; i < bmfr::kMaxFeatures; ++i) P.codes[i] = c->feature_buffers[i];
+    P.noise2 = c->noise_amount * (double)2.f;
+    P.blend_alpha = c->blend_alpha;
+    P.second_blend_alpha = c->second_blend_alpha;
+    P.taa_blend_alpha = c->taa_blend_alpha;
+    P.position_limit_sq = as_kernel_literal(c->position_limit_squared);
+    P.normal_limit_sq = as_kernel_literal(c->normal_limit_squared);
+    P.half_tmp = c->use_half_precision_in_tmp_data ? 1 : 0;
+    return P;
+}
+
+hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+bmfr::Camera make_camera(const float m[16], const float off[2]) {
+    bmfr::Camera cam;
+    for (int i = 0; i < 16; ++i) cam.m[i] = m[i];
+    cam.jx = off[0];
+    cam.jy = off[1];
+    return cam;
+}
+
+}  // namespace
+
+extern "C" {
+
+void bmfr_config_default(bmfr_config* c, int w, int h) {
+    std::memset(c, 0, sizeof *c);
+    c->image_width = w;
+    c->image_height = h;
+    // NOT_SCALED_FEATURE_BUFFERS / SCALED_FEATURE_BUFFERS, bmfr.cpp:65-77
+    const int f[] = {BMFR_FEATURE_ONE,        BMFR_FEATURE_NORMAL_X,   BMFR_FEATURE_NORMAL_Y,
+                     BMFR_FEATURE_NORMAL_Z,   BMFR_FEATURE_POSITION_X, BMFR_FEATURE_POSITION_Y,
+                     BMFR_FEATURE_POSITION_Z, BMFR_FEATURE_POSITION_X2, BMFR_FEATURE_POSITION_Y2,
+                     BMFR_FEATURE_POSITION_Z2};
+    c->features_not_scaled = 4;
+    c->features_scaled = 6;
+    for (int i = 0; i < 10; ++i) c->feature_buffers[i] = f[i];
+    c->noise_amount = 1e-2;          // bmfr.cpp:58
+    c->blend_alpha = 0.2f;           // bmfr.cpp:60
+    c->second_blend_alpha = 0.1f;    // bmfr.cpp:61
+    c->taa_blend_alpha = 0.2f;       // bmfr.cpp:62
+    c->position_limit_squared = 0.01;
+    c->normal_limit_squared = 0.1;
+    c->use_half_precision_in_tmp_data = 1;  // bmfr.cpp:88
+}
+
+bmfr_status bmfr_config_sizes(const bmfr_config* c, bmfr_sizes* s) {
+    const bmfr_status v = validate(c);
+    if (v != BMFR_OK) return v;
+    if (!s) return BMFR_ERROR_INVALID_ARGUMENT;
+    const int E = BMFR_BLOCK_EDGE_LENGTH;
+    s->buffer_count = c->features_not_scaled + c->features_scaled + 3;
+    s->r_edge = s->buffer_count - 2;
+    s->workset_width = E * ((c->image_width + E - 1) / E);
+    s->workset_height = E * ((c->image_height + E - 1) / E);
+    s->workset_with_margins_width = s->workset_width + E;
+    s->workset_with_margins_height = s->workset_height + E;
+    s->blocks = (s->workset_with_margins_width / E) * (s->workset_with_margins_height / E);
+    const size_t elem = c->use_half_precision_in_tmp_data ? 2 : 4;
+    s->tmp_data_bytes = (size_t)s->workset_with_margins_width * s->workset_with_margins_height *
+                        s->buffer_count * elem;
+    s->weights_bytes = (size_t)s->blocks * (s->buffer_count - 3) * 3 * sizeof(float);
+    s->mins_maxs_bytes = (size_t)s->blocks * c->features_scaled * 2 * sizeof(float);
+    s->image_bytes = (size_t)c->image_width * c->image_height * 3 * sizeof(float);
+    return BMFR_OK;
+}
+
+const char* bmfr_status_string(bmfr_status s) {
+    switch (s) {
+        case BMFR_OK: return "ok";
+        case BMFR_ERROR_INVALID_ARGUMENT: return "invalid argument";
+        case BMFR_ERROR_UNSUPPORTED: return "unsupported configuration";
+        case BMFR_ERROR_OUT_OF_MEMORY: return "out of device memory";
+        case BMFR_ERROR_HIP: return "HIP runtime error";
+        case BMFR_ERROR_NO_DEVICE: return "no HIP device";
+    }
+    return "unknown status";
+}
+
+int bmfr_last_hip_error(void) { return g_last_hip_error; }
+
+bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
+    if (!out) return BMFR_ERROR_INVALID_ARGUMENT;
+    *out = nullptr;
+    bmfr_sizes sz;
+    bmfr_status st = bmfr_config_sizes(cfg, &sz);
+    if (st != BMFR_OK) return st;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return BMFR_ERROR_NO_DEVICE;
+    if (device < 0 || device >= n) return BMFR_ERROR_NO_DEVICE;
+    st = hip_status(hipSetDevice(device));
+    if (st != BMFR_OK) return st;
+
+    bmfr_ctx* c = new bmfr_ctx;
+    c->cfg = *cfg;
+    c->sizes = sz;
+    c->P = make_params(cfg, &sz);
+    c->device = device;
+    const size_t px = (size_t)cfg->image_width * cfg->image_height;
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+        e = hipMalloc(&c->noisy_acc[i], px * 3 * sizeof(float));
+        if (e == hipSuccess) e = hipMalloc(&c->spp[i], px);
+        if (e == hipSuccess) e = hipMalloc(&c->acc[i], px * 3 * sizeof(float));
+        if (e == hipSuccess) e = hipMalloc(&c->result[i], px * 3 * sizeof(float));
+    }
+    if (e == hipSuccess) e = hipMalloc(&c->tone, px * 3 * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&c->prev_pixel, px * sizeof(float2));
+    if (e != hipSuccess) {
+        bmfr_destroy(c);
+        return hip_status(e);
+    }
+    *out = c;
+    return BMFR_OK;
+}
+
+bmfr_status bmfr_destroy(bmfr_ctx* c) {
+    if (!c) return BMFR_ERROR_INVALID_ARGUMENT;
+    for (int i = 0; i < 2; ++i) {
+        (void)hipFree(c->noisy_acc[i]);
+        (void)hipFree(c->spp[i]);
+        (void)hipFree(c->acc[i]);
+        (void)hipFree(c->result[i]);
+    }
+    if (c->prof_events)
+        for (int i = 0; i < 3 * c->prof_capacity; ++i) (void)hipEventDestroy(c->prof_events[i]);
+    delete[] c->prof_events;
+    delete[] c->prof_frames;
+    (void)hipFree(c->tone);
+    (void)hipFree(c->prev_pixel);
+    delete c;
+    return BMFR_OK;
+}
+
+bmfr_status bmfr_get_sizes(const bmfr_ctx* c, bmfr_sizes* out) {
+    if (!c || !out) return BMFR_ERROR_INVALID_ARGUMENT;
+    *out = c->sizes;
+    return BMFR_OK;
+}
+
+// ----------------------------------------------------------- stage API ----
+bmfr_status bmfr_accumulate_noisy_data(bmfr_ctx* c, void* stream, float* out_prev_frame_pixel,
+                                       uint8_t* accept_bools, const float* current_normals,
+                                       const float* previous_normals, const float* current_positions,
+                                       const float* previous_positions, float* current_noisy,
+                                       const float* previous_noisy, const uint8_t* previous_spp,
+                                       uint8_t* current_spp, void* tmp_data,
+                                       const float prev_frame_camera_matrix[16],
+                                       const float pixel_offset[2], int frame_number) {
+    if (!c || !out_prev_frame_pixel || !accept_bools || !current_normals || !current_positions ||
+        !current_noisy || !current_spp || !tmp_data || !prev_frame_camera_matrix || !pixel_offset ||
+        frame_number < 0)
+        return BMFR_ERROR_INVALID_ARGUMENT;
+    if (frame_number > 0 && (!previous_normals || !previous_positions || !previous_noisy || !previous_spp))
+        return BMFR_ERROR_INVALID_ARGUMENT;
+    bmfr::NoisyInputs in{current_normals, previous_normals, current_positions, previous_positions,
+                         current_noisy, previous_noisy, previous_spp};
+    return hip_status(bmfr::launch_accumulate_noisy(
+        c->P, as_stream(stream), reinterpret_cast<float2*>(out_prev_frame_pixel), accept_bools, in,
+        current_noisy, current_spp, tmp_data, make_camera(prev_frame_camera_matrix, pixel_offset),
+        frame_number));
+}
+
+bmfr_status bmfr_fitter(bmfr_ctx* c, void* stream, float* weights, float* mins_maxs, void* tmp_data,
+                        int frame_number) {
+    if (!c || !weights || !mins_maxs || !tmp_data || frame_number < 0) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (!bmfr::fitter_supported(c->P.not_scaled, c->P.scaled)) return BMFR_ERROR_UNSUPPORTED;
+    return hip_status(bmfr::launch_fitter(c->P, as_stream(stream), weights, mins_maxs, tmp_data, frame_number));
+}
+
+bmfr_status bmfr_weighted_sum(bmfr_ctx* c, void* stream, const float* weights, const float* mins_maxs,
+                              float* output, const float* current_normals,
+                              const float* current_positions, const float* current_noisy,
+                              int frame_number) {
+    (void)current_noisy;  // debugging-only argument upstream (bmfr.cl:709)
+    if (!c || !weights || !mins_maxs || !output || !current_normals || !current_positions || frame_number < 0)
+        return BMFR_ERROR_INVALID_ARGUMENT;
+    return hip_status(bmfr::launch_weighted_sum(c->P, as_stream(stream), weights, mins_maxs, output,
+                                                current_normals, current_positions, frame_number));
+}
+
+bmfr_status bmfr_accumulate_filtered_data(bmfr_ctx* c, void* stream, const float* filtered_frame,
+                                          const float* in_prev_frame_pixel, const uint8_t* accept_bools,
+                                          const float* albedo, float* tone_mapped_frame,
+                                          const uint8_t* current_spp, const float* accumulated_prev_frame,
+                                          float* accumulated_frame, int frame_number) {
+    if (!c || !filtered_frame || !in_prev_frame_pixel || !accept_bools || !albedo || !tone_mapped_frame ||
+        !current_spp || !accumulated_frame || frame_number < 0)
+        return BMFR_ERROR_INVALID_ARGUMENT;
+    if (frame_number > 0 && !accumulated_prev_frame) return BMFR_ERROR_INVALID_ARGUMENT;
+    return hip_status(bmfr::launch_accumulate_filtered(
+        c->P, as_stream(stream), filtered_frame, reinterpret_cast<const float2*>(in_prev_frame_pixel),
+        accept_bools, albedo, tone_mapped_frame, current_spp, accumulated_prev_frame, accumulated_frame,
+        frame_number));
+}
+
+bmfr_status bmfr_taa(bmfr_ctx* c, void* stream, const float* in_prev_frame_pixel, const float* new_frame,
+                     float* result_frame, const float* prev_frame, int frame_number) {
+    if (!c || !in_prev_frame_pixel || !new_frame || !result_frame || frame_number < 0)
+        return BMFR_ERROR_INVALID_ARGUMENT;
+    if (frame_number > 0 && !prev_frame) return BMFR_ERROR_INVALID_ARGUMENT;
+    return hip_status(bmfr::launch_taa(c->P, as_stream(stream),
+                                       reinterpret_cast<const float2*>(in_prev_frame_pixel), new_frame,
+                                       result_frame, prev_frame, frame_number));
+}
+
+// ----------------------------------------------------------- frame API ----
+bmfr_status bmfr_process_frame(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
+                               const float prev_frame_camera_matrix[16], const float pixel_offset[2],
+                               int frame_number) {
+    if (!c || !in || !in->noisy || !in->normals || !in->positions || !in->albedo ||
+        !prev_frame_camera_matrix || !pixel_offset || frame_number < 0)
+        return BMFR_ERROR_INVALID_ARGUMENT;
+    if (frame_number > 0 && (!in->prev_normals || !in->prev_positions || !c->has_frame))
+        return BMFR_ERROR_INVALID_ARGUMENT;
+    if (!bmfr::fitter_supported(c->P.not_scaled, c->P.scaled)) return BMFR_ERROR_UNSUPPORTED;
+    const int cur = c->has_frame ? 1 - c->cur : 0;  // swap, bmfr.cpp:482-484
+    const int prv = 1 - cur;
+    hipEvent_t* ev = nullptr;
+    if (c->prof_capacity > 0) {
+        const int slot = (int)(c->prof_count % c->prof_capacity);
+        ev = c->prof_events + 3 * slot;
+        c->prof_frames[slot] = frame_number;
+        (void)hipEventRecord(ev[0], as_stream(stream));
+    }
+    bmfr::FusedArgs A;
+    A.in = bmfr::NoisyInputs{in->normals, in->prev_normals, in->positions, in->prev_positions,
+                             in->noisy, c->noisy_acc[prv], c->spp[prv]};
+    A.cam = make_camera(prev_frame_camera_matrix, pixel_offset);
+    A.frame = frame_number;
+    A.albedo = in->albedo;
+    A.acc_prev = c->acc[prv];
+    A.result_prev = c->result[prv];
+    A.noisy_out = c->noisy_acc[cur];
+    A.spp_out = c->spp[cur];
+    A.prev_pixel_out = c->prev_pixel;
+    A.acc_out = c->acc[cur];
+    A.tone_out = c->tone;
+    A.result_out = c->result[cur];
+    const bmfr_status st = hip_status(bmfr::launch_fused_frame(c->P, as_stream(stream), A, ev ? ev[1] : nullptr));
+    if (st != BMFR_OK) return st;
+    if (ev) {
+        (void)hipEventRecord(ev[2], as_stream(stream));
+        ++c->prof_count;
+    }
+    c->cur = cur;
+    c->has_frame = true;
+    return BMFR_OK;
+}
+
+bmfr_status bmfr_set_profiling(bmfr_ctx* c, int enable, int capacity) {
+    if (!c || (enable && capacity <= 0)) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (c->prof_events) {
+        (void)hipDeviceSynchronize();
+        for (int i = 0; i < 3 * c->prof_capacity; ++i) (void)hipEventDestroy(c->prof_events[i]);
+        delete[] c->prof_events;
+        delete[] c->prof_frames;
+        c->prof_events = nullptr;
+        c->prof_frames = nullptr;
+    }
+    c->prof_capacity = 0;
+    c->prof_count = 0;
+    if (!enable) return BMFR_OK;
+    c->prof_events = new hipEvent_t[3 * capacity]();
+    c->prof_frames = new int[capacity]();
+    for (int i = 0; i < 3 * capacity; ++i) {
+        const bmfr_status st = hip_status(hipEventCreate(&c->prof_events[i]));
+        if (st != BMFR_OK) return st;
+    }
+    c->prof_capacity = capacity;
+    return BMFR_OK;
+}
+
+bmfr_status bmfr_get_profile(bmfr_ctx* c, bmfr_frame_profile* out, int max_frames, int* count) {
+    if (!c || !count || (max_frames > 0 && !out)) return BMFR_ERROR_INVALID_ARGUMENT;
+    const long have = c->prof_count < c->prof_capacity ? c->prof_count : c->prof_capacity;
+    const long first = c->prof_count - have;
+    int n = 0;
+    for (long k = first; k < c->prof_count && n < max_frames; ++k, ++n) {
+        const int slot = (int)(k % c->prof_capacity);
+        hipEvent_t* ev = c->prof_events + 3 * slot;
+        bmfr_status st = hip_status(hipEventSynchronize(ev[2]));
+        if (st != BMFR_OK) return st;
+        float a = 0, b = 0, t = 0;
+        if ((st = hip_status(hipEventElapsedTime(&a, ev[0], ev[1]))) != BMFR_OK) return st;
+        if ((st = hip_status(hipEventElapsedTime(&b, ev[1], ev[2]))) != BMFR_OK) return st;
+        if ((st = hip_status(hipEventElapsedTime(&t, ev[0], ev[2]))) != BMFR_OK) return st;
+        out[n].frame_number = c->prof_frames[slot];
+        out[n].fused_block_ms = a;
+        out[n].taa_ms = b;
+        out[n].total_ms = t;
+    }
+    *count = n;
+    return BMFR_OK;
+}
+
+const float* bmfr_output(const bmfr_ctx* c) {
+    if (!c || !c->has_frame) return nullptr;
+    return c->result[c->cur];
+}
+
+bmfr_status bmfr_state(const bmfr_ctx* c, int previous, bmfr_state_view* out) {
+    if (!c || !out) return BMFR_ERROR_INVALID_ARGUMENT;
+    const int i = previous ? 1 - c->cur : c->cur;
+    out->noisy_accumulated = c->noisy_acc[i];
+    out->spp = c->spp[i];
+    out->filtered_accumulated = c->acc[i];
+    out->tone_mapped = c->tone;
+    out->prev_frame_pixel = reinterpret_cast<float*>(c->prev_pixel);
+    out->accept = nullptr;  // the fused kernel keeps accept bits in registers
+    out->result = c->result[i];
+    return BMFR_OK;
+}
+
+}  // extern "C"

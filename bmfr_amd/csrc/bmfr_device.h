@@ -1,0 +1,117 @@
+// bmfr_device.h -- device-side building blocks of the BMFR kernels (gfx950).
+//
+// Arithmetic contract: every helper here rounds exactly like the reference
+// kernels in /root/reference/opencl/bmfr.cl do when compiled for gfx950 with
+// IEEE-strict OpenCL options (no contraction of user code, correctly rounded
+// division and sqrt).  The library is built with -ffp-contract=off, so an
+// expression `a * b + c` is two rounded operations; __builtin_fmaf appears
+// only where the reference's OpenCL library itself fuses (dot(), whose ROCm
+// device-libs implementation is an fmuladd chain).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bmfr_params.h"
+
+namespace bmfr {
+
+// BLOCK_OFFSETS, bmfr.cl:267-285: per-frame shift of the 32x32 block grid.
+__constant__ static const int2 kBlockOffsets[16] = {
+    {-14, -14}, {4, -6}, {-8, 14}, {8, 0}, {-10, -8}, {2, 12}, {12, -12}, {-10, 0},
+    {12, 14}, {-8, -16}, {6, 6}, {-2, -2}, {6, -14}, {-16, 12}, {14, -4}, {-6, 4}};
+
+struct f3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ f3 ld3(const float* __restrict__ b, long i) {
+    return f3{b[3 * i], b[3 * i + 1], b[3 * i + 2]};
+}
+__device__ __forceinline__ void st3(float* __restrict__ b, long i, f3 v) {
+    b[3 * i] = v.x;
+    b[3 * i + 1] = v.y;
+    b[3 * i + 2] = v.z;
+}
+
+// OpenCL dot() as ROCm's opencl.bc implements it (fmuladd chain).
+__device__ __forceinline__ float dot3(f3 a, f3 b) {
+    return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
+}
+__device__ __forceinline__ float dot4(float a0, float a1, float a2, float a3, float b0, float b1,
+                                      float b2, float b3) {
+    return __builtin_fmaf(a3, b3, __builtin_fmaf(a2, b2, __builtin_fmaf(a1, b1, a0 * b0)));
+}
+
+// mirror(), bmfr.cl:207-216.
+__device__ __forceinline__ int mirror(int i, int size) {
+    return i < 0 ? -i - 1 : (i >= size ? 2 * size - i - 1 : i);
+}
+
+// scale(), bmfr.cl:200-205.
+__device__ __forceinline__ float scale(float v, float mn, float mx) {
+    const float d = mx - mn;
+    return fabsf(d) > 1.0f ? (v - mn) / d : v - mn;
+}
+
+// vstore_half / vload_half round trip (round to nearest even), bmfr.cl:255-258.
+__device__ __forceinline__ float round_half(float v) { return (float)(_Float16)v; }
+
+// random() + add_random(), bmfr.cl:161-182.  NOISE_AMOUNT is a double
+// literal upstream, so the noise and the add are double.
+__device__ __forceinline__ float hash_random(uint32_t a) {
+    a = (a + 0x7ed55d16u) + (a << 12);
+    a = (a ^ 0xc761c23cu) ^ (a >> 19);
+    a = (a + 0x165667b1u) + (a << 5);
+    a = (a + 0xd3a2646cu) ^ (a << 9);
+    a = (a + 0xfd7046c5u) + (a << 3);
+    a = (a ^ 0xb55a4f09u) ^ (a >> 16);
+    return (float)a / 4294967296.0f;  // convert_float(UINT_MAX) == 2^32
+}
+__device__ __forceinline__ float add_random(float v, double noise2, int seed) {
+    const float r = hash_random((uint32_t)seed) - 0.5f;
+    return (float)((double)v + noise2 * (double)r);
+}
+
+// One FEATURE_BUFFERS entry (bmfr.cl:448-453, 727-729).
+__device__ __forceinline__ float feature_value(int code, f3 n, f3 p) {
+    switch (code) {
+        case kFeatOne: return 1.f;
+        case kFeatNx: return n.x;
+        case kFeatNy: return n.y;
+        case kFeatNz: return n.z;
+        case kFeatPx: return p.x;
+        case kFeatPy: return p.y;
+        case kFeatPz: return p.z;
+        case kFeatPx2: return p.x * p.x;
+        case kFeatPy2: return p.y * p.y;
+        case kFeatPz2: return p.z * p.z;
+        case kFeatPx3: return p.x * p.x * p.x;
+        case kFeatPy3: return p.y * p.y * p.y;
+        case kFeatPz3: return p.z * p.z * p.z;
+        default: return 0.f;
+    }
+}
+
+// RGB <-> YCoCg, bmfr.cl:184-198 (dot-based, hence fma chains).
+__device__ __forceinline__ f3 rgb_to_ycocg(f3 c) {
+    return f3{dot3(c, f3{1.f, 2.f, 1.f}), dot3(c, f3{2.f, 0.f, -2.f}), dot3(c, f3{-1.f, 2.f, -1.f})};
+}
+__device__ __forceinline__ f3 ycocg_to_rgb(f3 c) {
+    return f3{dot3(c, f3{0.25f, 0.25f, -0.25f}), dot3(c, f3{0.25f, 0.f, 0.25f}),
+              dot3(c, f3{0.25f, -0.25f, -0.25f})};
+}
+
+extern "C" __device__ float __ocml_powr_f32(float, float);
+
+// Correctly rounded a / b given y = RN(1/b): one Markstein correction step
+// (r = a - q*b is exact under FMA; q + r*y rounds to RN(a/b) for normal
+// operands).  Used where one divisor serves many dividends (the fitter's
+// trailing update), in place of the ~10-instruction generic division.
+__device__ __forceinline__ float div_by_recip(float a, float b, float y) {
+    const float q = a * y;
+    const float r = __builtin_fmaf(-q, b, a);
+    return __builtin_fmaf(r, y, q);
+}
+
+}  // namespace bmfr

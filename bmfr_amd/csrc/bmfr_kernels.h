@@ -1,0 +1,388 @@
+// bmfr_kernels.h -- device building blocks shared by the stage kernels and
+// the fused frame kernels (bmfr_kernels.hip).
+//
+// Fitter work decomposition: one 256-thread work-group per 32x32 block, as
+// upstream (bmfr.cl:487-501), but the block's whole design matrix lives in
+// VGPRs: thread t owns rows t + 256*s (s = 0..3) of every column, i.e. the
+// rows upstream work-item t touches, so the per-thread partial sums and the
+// 256->64->8->1 reduction tree can be reproduced in the reference's exact
+// association while tmp_data is read from HBM once instead of once per
+// Householder column (bmfr.cl:555-656 re-reads it every pass).
+#pragma once
+
+#include "bmfr_device.h"
+
+namespace bmfr {
+
+// --------------------------------------------------------------------------
+// Batched block reductions with the association of bmfr.cl:25-87.
+// `v[k]` is work-item t's partial of reduction k (k < n, n <= K).  The result
+// of reduction k lands in res[k]; all threads may read it on return.
+// --------------------------------------------------------------------------
+enum class RedOp { Sum, Max, Min };
+
+template <RedOp OP>
+__device__ __forceinline__ float red(float a, float b) {
+    if constexpr (OP == RedOp::Sum) return a + b;
+    else if constexpr (OP == RedOp::Max) return fmaxf(a, b);
+    else return fminf(a, b);
+}
+
+template <RedOp OP>
+__device__ __forceinline__ float bcast_lane(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+template <RedOp OP, int K>
+__device__ __forceinline__ void block_reduce(const float (&v)[K], int n, float* __restrict__ part,
+                                             float* __restrict__ res, int t) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (k < n) part[k * kLocal + t] = v[k];
+    __syncthreads();
+    const int w = t >> 6, l = t & 63;
+#pragma unroll
+    for (int i = 0; i < (K + 3) / 4; ++i) {
+        const int k = w + 4 * i;
+        if (k < n) {  // wave-uniform
+            const float* p = part + k * kLocal;
+            // 256 -> 64 (bmfr.cl:32-33 / 51-53 / 73-75)
+            float s;
+            if constexpr (OP == RedOp::Sum) s = p[l] + ((p[l + 64] + p[l + 128]) + p[l + 192]);
+            else s = red<OP>(red<OP>(red<OP>(p[l], p[l + 64]), p[l + 128]), p[l + 192]);
+            // 64 -> 8 (bmfr.cl:35-37 / 55-58 / 77-80), computed on lanes 0..7
+            float e;
+            if constexpr (OP == RedOp::Sum) {
+                float acc = __shfl(s, (l + 8) & 63);
+#pragma unroll
+                for (int j = 2; j < 8; ++j) acc = acc + __shfl(s, (l + 8 * j) & 63);
+                e = s + acc;
+            } else {
+                e = s;
+#pragma unroll
+                for (int j = 1; j < 8; ++j) e = red<OP>(e, __shfl(s, (l + 8 * j) & 63));
+            }
+            // 8 -> 1 (bmfr.cl:39-42), left to right
+            float r = bcast_lane<OP>(e, 0);
+#pragma unroll
+            for (int j = 1; j < 8; ++j) r = red<OP>(r, bcast_lane<OP>(e, j));
+            if (l == 0) res[k] = r;
+        }
+    }
+    __syncthreads();
+}
+
+// --------------------------------------------------------------------------
+// accumulate_noisy_data for one work-item of the margin grid (bmfr.cl:310-476).
+// --------------------------------------------------------------------------
+struct NoisyItem {
+    f3 n, p;          // current normal / world position of the (mirrored) pixel
+    f3 color;         // blended colour (features B-3..B-1)
+    float pfx, pfy;   // prev_frame_pixel_f
+    long lin;         // linear (mirrored) pixel
+    uint8_t accept;
+    uint8_t spp;
+    bool owner;       // pixel_without_mirror inside the image
+};
+
+struct NoisyInputs {
+    const float* __restrict__ n_cur;
+    const float* __restrict__ n_prev;
+    const float* __restrict__ p_cur;
+    const float* __restrict__ p_prev;
+    const float* noisy_cur;  // may alias the stage kernel's output (in-place, bmfr.cl:297)
+    const float* __restrict__ noisy_prev;
+    const uint8_t* __restrict__ spp_prev;
+};
+
+struct Camera {
+    float m[16];   // previous frame's VP, column-major
+    float jx, jy;  // this frame's pixel offset
+};
+
+__device__ __forceinline__ NoisyItem noisy_item(const Params& P, const NoisyInputs& in,
+                                                const Camera& cam, int gx, int gy, int frame) {
+    NoisyItem o;
+    const int2 off = kBlockOffsets[frame & 15];
+    const int ux = gx - kEdge / 2 + off.x, uy = gy - kEdge / 2 + off.y;
+    const int px = mirror(ux, P.width), py = mirror(uy, P.height);
+    o.owner = ux >= 0 && ux < P.width && uy >= 0 && uy < P.height;
+    o.lin = (long)py * P.width + px;
+
+    const f3 wp = ld3(in.p_cur, o.lin);
+    const f3 nrm = ld3(in.n_cur, o.lin);
+    const f3 cur = ld3(in.noisy_cur, o.lin);
+    o.n = nrm;
+    o.p = wp;
+
+    float pfx = (float)px, pfy = (float)py;
+    uint8_t accept = 0;
+    float alpha = 1.f;
+    f3 prev{0.f, 0.f, 0.f};
+    float sample_spp = 0.f;
+    if (frame > 0) {
+        const float* M = cam.m;
+        // .s048c / .s159d / .s37bf rows of the column-major matrix (bmfr.cl:343-347)
+        float u = dot4(M[0], M[4], M[8], M[12], wp.x, wp.y, wp.z, 1.f);
+        float v = dot4(M[1], M[5], M[9], M[13], wp.x, wp.y, wp.z, 1.f);
+        const float w = dot4(M[3], M[7], M[11], M[15], wp.x, wp.y, wp.z, 1.f);
+        u = u / w;
+        v = v / w;
+        u = u + 1.f;
+        v = v + 1.f;
+        u = u / 2.f;
+        v = v / 2.f;
+        pfx = u * (float)P.width - cam.jx;
+        pfy = v * (float)P.height - (1 - cam.jy);
+        const float flx = floorf(pfx), fly = floorf(pfy);
+        const int ix = (int)flx, iy = (int)fly;
+        const float fx = pfx - flx, fy = pfy - fly;
+        const float omx = 1.f - fx, omy = 1.f - fy;
+        const float wts[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
+        float total = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // bmfr.cl:374-419
+            const int sx = ix + (i & 1), sy = iy + (i >> 1);
+            if (sx >= 0 && sy >= 0 && sx < P.width && sy < P.height) {
+                const long s = (long)sy * P.width + sx;
+                const f3 pp = ld3(in.p_prev, s);
+                const f3 d{pp.x - wp.x, pp.y - wp.y, pp.z - wp.z};
+                if (dot3(d, d) < P.position_limit_sq) {
+                    const f3 pn = ld3(in.n_prev, s);
+                    const f3 dn{pn.x - nrm.x, pn.y - nrm.y, pn.z - nrm.z};
+                    if (dot3(dn, dn) < P.normal_limit_sq) {
+                        accept |= (uint8_t)(1 << i);
+                        sample_spp = sample_spp + wts[i] * (float)in.spp_prev[s];
+                        const f3 pc = ld3(in.noisy_prev, s);
+                        prev.x = prev.x + wts[i] * pc.x;
+                        prev.y = prev.y + wts[i] * pc.y;
+                        prev.z = prev.z + wts[i] * pc.z;
+                        total = total + wts[i];
+                    }
+                }
+            }
+        }
+        if (total > 0.f) {  // bmfr.cl:421-429
+            prev.x = prev.x / total;
+            prev.y = prev.y / total;
+            prev.z = prev.z / total;
+            sample_spp = sample_spp / total;
+            alpha = 1.f / (sample_spp + 1.f);
+            alpha = fmaxf(alpha, P.blend_alpha);
+        }
+    }
+    uint8_t new_spp = 1;  // bmfr.cl:433-442
+    if (alpha < 1.f) new_spp = sample_spp > 254.f ? 255 : (uint8_t)((int)rintf(sample_spp) + 1);
+    const float beta = 1.f - alpha;
+    o.color = f3{alpha * cur.x + beta * prev.x, alpha * cur.y + beta * prev.y,
+                 alpha * cur.z + beta * prev.z};
+    o.pfx = pfx;
+    o.pfy = pfy;
+    o.accept = accept;
+    o.spp = new_spp;
+    return o;
+}
+
+// tmp_data value of feature f for an item (bmfr.cl:448-473): NaN -> 0, and
+// the +-65504 clamp when the matrix is kept in half.
+__device__ __forceinline__ float design_value(const Params& P, int f, const NoisyItem& it) {
+    const int B = P.buffers;
+    float v;
+    if (f < B - 3) v = feature_value(P.codes[f], it.n, it.p);
+    else v = f == B - 3 ? it.color.x : (f == B - 2 ? it.color.y : it.color.z);
+    if (__builtin_isnan(v)) v = 0.0f;
+    if (P.half_tmp) v = fmaxf(fminf(v, 65504.f), -65504.f);
+    return v;
+}
+
+// --------------------------------------------------------------------------
+// The fitter (bmfr.cl:503-699) on a register-resident block.
+//   a[f][s]  : row t + 256*s of feature column f (rounded to half if HALF)
+//   FULL     : also run the colour columns' own Householder steps, which only
+//              touch rows >= B-3 and the never-read slot R(R_EDGE-1,R_EDGE-1)
+//              (bmfr.cl:550,606); needed only to leave tmp_data exactly as
+//              upstream does.  The fused kernel skips them.
+//   FAST_DIV : trailing update divides through div_by_recip (bit-identical
+//              to the correctly rounded quotient; see bmfr_device.h).
+// On return lds.weights[(B-3)*3] holds the block's weights and
+// lds.minmax[FS*2] its min/max (mins_maxs layout).
+// --------------------------------------------------------------------------
+template <int B>
+struct FitLds {
+    float part[(B - 1) * kLocal];
+    float res[B];
+    float bc[2];
+    float R[(B - 2) * (B - 2) * 3];  // R[x][y][ch], x = column, y = row
+    float weights[(B - 3) * 3];
+    float minmax[2 * (B - 3)];
+};
+
+template <int NS, int FS, bool HALF, bool FULL, bool FAST_DIV>
+__device__ __forceinline__ void fit_block(float (&a)[NS + FS + 3][kSubs], FitLds<NS + FS + 3>& L,
+                                          int t, int frame, double noise2) {
+    constexpr int B = NS + FS + 3;
+    constexpr int RE = B - 2;  // R_EDGE
+
+    // Scale the position features to the block's [min, max] (bmfr.cl:510-542).
+    if constexpr (FS > 0) {
+        float mx[FS], mn[FS];
+#pragma unroll
+        for (int f = 0; f < FS; ++f) {
+            float hi = -INFINITY, lo = INFINITY;
+#pragma unroll
+            for (int s = 0; s < kSubs; ++s) {
+                hi = fmaxf(a[NS + f][s], hi);
+                lo = fminf(a[NS + f][s], lo);
+            }
+            mx[f] = hi;
+            mn[f] = lo;
+        }
+        block_reduce<RedOp::Max, FS>(mx, FS, L.part, L.res, t);
+        float bmax[FS];
+#pragma unroll
+        for (int f = 0; f < FS; ++f) bmax[f] = L.res[f];
+        block_reduce<RedOp::Min, FS>(mn, FS, L.part, L.res, t);
+#pragma unroll
+        for (int f = 0; f < FS; ++f) {
+            const float bmin = L.res[f];
+            if (t == 0) {
+                L.minmax[2 * f] = bmin;
+                L.minmax[2 * f + 1] = bmax[f];
+            }
+#pragma unroll
+            for (int s = 0; s < kSubs; ++s) {
+                const float v = scale(a[NS + f][s], bmin, bmax[f]);
+                a[NS + f][s] = HALF ? round_half(v) : v;
+            }
+        }
+    }
+
+    // Householder QR (bmfr.cl:544-656).
+    constexpr int COLS = FULL ? B : B - 3;
+#pragma unroll
+    for (int col = 0; col < COLS; ++col) {
+        constexpr int dummy = 0;
+        (void)dummy;
+        const int cl = col < B - 3 ? col : B - 3;  // col_limited
+        float sq = 0.f;
+#pragma unroll
+        for (int s = 0; s < kSubs; ++s) {
+            const int i = t + s * kLocal;
+            if (i >= cl + 1) sq = sq + a[col][s] * a[col][s];
+        }
+        if (t == cl) L.bc[0] = a[col][0];  // u_vec[col_limited], row cl is row t=cl, s=0
+        {
+            float one[1] = {sq};
+            block_reduce<RedOp::Sum, 1>(one, 1, L.part, L.res, t);
+        }
+        const float sumsq = L.res[0];
+        const float ucl = L.bc[0];
+        const float vlen = sqrtf(sumsq + ucl * ucl);  // bmfr.cl:582-585
+        const float ucl2 = ucl - vlen;
+        const float ulen2 = sumsq + ucl2 * ucl2;
+
+        // R column (bmfr.cl:574-601).  Rows y < col belong to thread y, s = 0.
+        if (col < B - 3) {
+            if (t < col) {
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) L.R[(col * RE + t) * 3 + ch] = a[col][0];
+            }
+            if (t == col) {
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) L.R[(col * RE + col) * 3 + ch] = vlen;
+            }
+        } else {
+            if (t < B - 3) L.R[((RE - 1) * RE + t) * 3 + (col - (B - 3))] = a[col][0];
+        }
+
+        float u[kSubs];
+#pragma unroll
+        for (int s = 0; s < kSubs; ++s) u[s] = a[col][s];
+        if (t == cl) u[0] = ucl2;
+
+        // Trailing columns fb = cl+1 .. B-1 (bmfr.cl:606-655): all dots first
+        // (one batched reduction), then all updates.  Each column's update only
+        // depends on its own dot, so the per-element arithmetic is upstream's.
+        float dp[B - 1];
+#pragma unroll
+        for (int fb = 1; fb < B; ++fb) {
+            float d = 0.f;
+            if (fb > cl) {
+#pragma unroll
+                for (int s = 0; s < kSubs; ++s) {
+                    const int i = t + s * kLocal;
+                    if (i >= cl) {
+                        float v = a[fb][s];
+                        if (col == 0 && fb < B - 3)  // noise once, on first load (bmfr.cl:625-627)
+                            v = add_random(v, noise2, t + s * kLocal + fb * kBlockPixels +
+                                                          frame * B * kBlockPixels);
+                        a[fb][s] = v;
+                        d = d + v * u[s];
+                    }
+                }
+            }
+            dp[fb - 1] = d;
+        }
+        // Reduction k covers column fb = cl + 1 + k.
+        float dk[B - 1];
+#pragma unroll
+        for (int k = 0; k < B - 1; ++k) dk[k] = 0.f;
+#pragma unroll
+        for (int fb = 1; fb < B; ++fb)
+            if (fb > cl) dk[fb - cl - 1] = dp[fb - 1];
+        block_reduce<RedOp::Sum, B - 1>(dk, B - 1 - cl, L.part, L.res, t);
+
+        const float recip = 1.f / ulen2;
+#pragma unroll
+        for (int fb = 1; fb < B; ++fb) {
+            if (fb > cl) {
+                const float c2 = 2.f * L.res[fb - cl - 1];  // 2*u*dot == u*(2*dot), both exact doublings
+#pragma unroll
+                for (int s = 0; s < kSubs; ++s) {
+                    const int i = t + s * kLocal;
+                    if (i >= cl) {
+                        const float num = u[s] * c2;
+                        const float q = FAST_DIV ? div_by_recip(num, ulen2, recip) : num / ulen2;
+                        const float v = a[fb][s] - q;
+                        a[fb][s] = HALF ? round_half(v) : v;
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (!FULL) {
+        // Right-hand side = rows 0..B-4 of the colour columns, untouched by the
+        // colour columns' own steps (they only write rows >= B-3).
+        if (t < B - 3) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) L.R[((RE - 1) * RE + t) * 3 + ch] = a[B - 3 + ch][0];
+        }
+    }
+    __syncthreads();
+
+    // Back substitution (bmfr.cl:658-699), one lane per colour channel.  Each
+    // element sees upstream's operations in upstream's order.
+    if (t < 3) {
+        const int ch = t;
+        float R[RE][RE];
+#pragma unroll
+        for (int x = 0; x < RE; ++x)
+#pragma unroll
+            for (int y = 0; y <= (x < RE - 1 ? x : RE - 2); ++y) R[x][y] = L.R[(x * RE + y) * 3 + ch];
+#pragma unroll
+        for (int i = RE - 2; i >= 0; --i) {
+            const float div = R[i][i];
+#pragma unroll
+            for (int x = i; x < RE; ++x) R[x][i] = R[x][i] / div;
+#pragma unroll
+            for (int j = i + 1; j < RE - 1; ++j) R[RE - 1][i] = R[RE - 1][i] - R[j][i];
+#pragma unroll
+            for (int y = 0; y <= i; ++y) R[i][y] = R[i][y] * R[RE - 1][i];
+        }
+#pragma unroll
+        for (int id = 0; id < B - 3; ++id) L.weights[id * 3 + ch] = R[RE - 1][id];
+    }
+    __syncthreads();
+}
+
+}  // namespace bmfr

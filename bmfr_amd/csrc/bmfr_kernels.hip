@@ -1,0 +1,392 @@
+// bmfr_kernels.hip -- BMFR kernels for MI355X (gfx950).
+//
+// Two families:
+//  * Stage kernels: one per reference kernel, same buffer layouts and
+//    argument roles (bmfr.cl:290-974).  They back the stage C-ABI entry
+//    points and the per-stage parity tests.
+//  * Fused frame kernels: K1 = accumulate_noisy -> scale -> QR -> solve ->
+//    weighted_sum -> accumulate_filtered -> tone map for one 32x32 block per
+//    256-thread work-group, with the design matrix never leaving VGPRs
+//    (upstream round-trips it through HBM ~30 times per block, bmfr.cl:555-656);
+//    K2 = TAA (needs the 3x3 neighbourhood across block borders).
+#include "bmfr_kernels.h"
+#include "bmfr_launch.h"
+
+namespace bmfr {
+
+// ---------------------------------------------------------------- stage 1 --
+// pass 0: margin work-items only, pass 1: owners only.  Launched in that
+// order, every read of current_noisy sees the input colour.
+__global__ __launch_bounds__(256) void k_accumulate_noisy(Params P, NoisyInputs in, Camera cam,
+                                                          int frame, int pass, float2* prev_pixel,
+                                                          uint8_t* accept, float* noisy_out,
+                                                          uint8_t* spp_cur, void* tmp) {
+    const int gx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int gy = blockIdx.y * blockDim.y + threadIdx.y;
+    if (gx >= P.margins_w || gy >= P.margins_h) return;
+    const int2 off = kBlockOffsets[frame & 15];
+    const int ux = gx - kEdge / 2 + off.x, uy = gy - kEdge / 2 + off.y;
+    const bool owner = ux >= 0 && ux < P.width && uy >= 0 && uy < P.height;
+    if ((int)owner != pass) return;
+
+    const NoisyItem it = noisy_item(P, in, cam, gx, gy, frame);
+    spp_cur[it.lin] = it.spp;
+    const int bx = gx / kEdge, by = gy / kEdge;
+    const size_t base = ((size_t)by * P.blocks_x + bx) * (size_t)P.buffers * kBlockPixels +
+                        (size_t)(gy % kEdge) * kEdge + (gx % kEdge);
+    for (int f = 0; f < P.buffers; ++f) {
+        const float v = design_value(P, f, it);
+        if (P.half_tmp) ((_Float16*)tmp)[base + (size_t)f * kBlockPixels] = (_Float16)v;
+        else ((float*)tmp)[base + (size_t)f * kBlockPixels] = v;
+    }
+    if (it.owner) {
+        st3(noisy_out, it.lin, it.color);
+        prev_pixel[it.lin] = make_float2(it.pfx, it.pfy);
+        accept[it.lin] = it.accept;
+    }
+}
+
+// ---------------------------------------------------------------- stage 2 --
+template <int NS, int FS, bool HALF>
+__global__ __launch_bounds__(256) void k_fitter(Params P, float* __restrict__ weights,
+                                                float* __restrict__ mins_maxs, void* tmp, int frame) {
+    constexpr int B = NS + FS + 3;
+    __shared__ FitLds<B> L;
+    const int t = threadIdx.x, g = blockIdx.x;
+    const size_t base = (size_t)g * B * kBlockPixels;
+    float a[B][kSubs];
+#pragma unroll
+    for (int f = 0; f < B; ++f)
+#pragma unroll
+        for (int s = 0; s < kSubs; ++s) {
+            const size_t i = base + (size_t)f * kBlockPixels + t + s * kLocal;
+            a[f][s] = HALF ? (float)((const _Float16*)tmp)[i] : ((const float*)tmp)[i];
+        }
+    fit_block<NS, FS, HALF, true, false>(a, L, t, frame, P.noise2);
+#pragma unroll
+    for (int f = 0; f < B; ++f)
+#pragma unroll
+        for (int s = 0; s < kSubs; ++s) {
+            const size_t i = base + (size_t)f * kBlockPixels + t + s * kLocal;
+            if (HALF) ((_Float16*)tmp)[i] = (_Float16)a[f][s];
+            else ((float*)tmp)[i] = a[f][s];
+        }
+    if (t < (B - 3) * 3) weights[(size_t)g * (B - 3) * 3 + t] = L.weights[t];
+    if (t < FS * 2) mins_maxs[(size_t)g * FS * 2 + t] = L.minmax[t];
+}
+
+// ---------------------------------------------------------------- stage 3 --
+// Features recomputed in f32 from normals/positions, scaled with the block's
+// min/max, dotted with the block's weights (bmfr.cl:703-758).
+__device__ __forceinline__ f3 weighted_color(const Params& P, const float* __restrict__ w,
+                                             const float* __restrict__ mm, f3 n, f3 p) {
+    f3 c{0.f, 0.f, 0.f};
+    for (int f = 0; f < P.buffers - 3; ++f) {
+        float v = feature_value(P.codes[f], n, p);
+        if (f >= P.not_scaled) v = scale(v, mm[2 * (f - P.not_scaled)], mm[2 * (f - P.not_scaled) + 1]);
+        c.x = c.x + w[3 * f] * v;
+        c.y = c.y + w[3 * f + 1] * v;
+        c.z = c.z + w[3 * f + 2] * v;
+    }
+    c.x = c.x < 0.f ? 0.f : c.x;
+    c.y = c.y < 0.f ? 0.f : c.y;
+    c.z = c.z < 0.f ? 0.f : c.z;
+    return c;
+}
+
+__device__ __forceinline__ int block_of_pixel(const Params& P, int x, int y, int frame) {
+    const int2 off = kBlockOffsets[frame & 15];
+    return (x + kEdge / 2 - off.x) / kEdge + ((y + kEdge / 2 - off.y) / kEdge) * P.blocks_x;
+}
+
+__global__ __launch_bounds__(256) void k_weighted_sum(Params P, const float* __restrict__ weights,
+                                                      const float* __restrict__ mins_maxs,
+                                                      float* __restrict__ out,
+                                                      const float* __restrict__ normals,
+                                                      const float* __restrict__ positions, int frame) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y * blockDim.y + threadIdx.y;
+    if (x >= P.width || y >= P.height) return;
+    const long lin = (long)y * P.width + x;
+    const int g = block_of_pixel(P, x, y, frame);
+    const f3 c = weighted_color(P, weights + (size_t)g * (P.buffers - 3) * 3,
+                                mins_maxs + (size_t)g * P.scaled * 2, ld3(normals, lin),
+                                ld3(positions, lin));
+    st3(out, lin, c);
+}
+
+// ---------------------------------------------------------------- stage 4 --
+// Temporal blend of the filtered colour, albedo remodulation and the
+// 1/2.2 gamma (bmfr.cl:761-857).  Returns the accumulated colour; *tone gets
+// the tone-mapped one.
+__device__ __forceinline__ f3 accumulate_filtered(const Params& P, f3 filtered, float pfx, float pfy,
+                                                  uint8_t acc_bits, uint8_t spp, f3 albedo,
+                                                  const float* __restrict__ acc_prev, int frame,
+                                                  f3* tone) {
+    f3 prev{0.f, 0.f, 0.f};
+    float alpha = 1.f;
+    if (frame > 0 && acc_bits > 0) {
+        const float flx = floorf(pfx), fly = floorf(pfy);
+        const int ix = (int)flx, iy = (int)fly;
+        const float fx = pfx - flx, fy = pfy - fly;
+        const float omx = 1.f - fx, omy = 1.f - fy;
+        const float wts[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
+        float total = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (acc_bits & (1 << i)) {
+                total = total + wts[i];
+                const f3 pc = ld3(acc_prev, (long)(iy + (i >> 1)) * P.width + ix + (i & 1));
+                prev.x = prev.x + wts[i] * pc.x;
+                prev.y = prev.y + wts[i] * pc.y;
+                prev.z = prev.z + wts[i] * pc.z;
+            }
+        }
+        if (total > 0.f) {
+            alpha = 1.f / (float)spp;
+            alpha = fmaxf(alpha, P.second_blend_alpha);
+            prev.x = prev.x / total;
+            prev.y = prev.y / total;
+            prev.z = prev.z / total;
+        }
+    }
+    const float beta = 1.f - alpha;
+    const f3 a{alpha * filtered.x + beta * prev.x, alpha * filtered.y + beta * prev.y,
+               alpha * filtered.z + beta * prev.z};
+    const float g = 0.454545f;
+    tone->x = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.x * a.x), g), 0.f), 1.f);
+    tone->y = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.y * a.y), g), 0.f), 1.f);
+    tone->z = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.z * a.z), g), 0.f), 1.f);
+    return a;
+}
+
+__global__ __launch_bounds__(256) void k_accumulate_filtered(
+    Params P, const float* __restrict__ filtered, const float2* __restrict__ prev_pixel,
+    const uint8_t* __restrict__ accept, const float* __restrict__ albedo,
+    float* __restrict__ tone_mapped, const uint8_t* __restrict__ spp,
+    const float* __restrict__ acc_prev, float* __restrict__ acc, int frame) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y * blockDim.y + threadIdx.y;
+    if (x >= P.width || y >= P.height) return;
+    const long lin = (long)y * P.width + x;
+    const float2 pp = prev_pixel[lin];
+    f3 tone;
+    const f3 a = accumulate_filtered(P, ld3(filtered, lin), pp.x, pp.y, frame > 0 ? accept[lin] : 0,
+                                     spp[lin], ld3(albedo, lin), acc_prev, frame, &tone);
+    st3(acc, lin, a);
+    st3(tone_mapped, lin, tone);
+}
+
+// ---------------------------------------------------------------- stage 5 --
+__global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict__ prev_pixel,
+                                             const float* __restrict__ new_frame,
+                                             float* __restrict__ result,
+                                             const float* __restrict__ prev_frame, int frame) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y * blockDim.y + threadIdx.y;
+    if (x >= P.width || y >= P.height) return;
+    const int W = P.width, H = P.height;
+    const long lin = (long)y * W + x;
+    const f3 me = ld3(new_frame, lin);
+    const float2 pf = prev_pixel[lin];
+    const float flx = floorf(pf.x), fly = floorf(pf.y);
+    const int ix = (int)flx, iy = (int)fly;
+    if (frame == 0 || ix < -1 || iy < -1 || ix >= W || iy >= H) {  // bmfr.cl:884-890
+        st3(result, lin, me);
+        return;
+    }
+    f3 mnb{INFINITY, INFINITY, INFINITY}, mnc = mnb;
+    f3 mxb{-INFINITY, -INFINITY, -INFINITY}, mxc = mxb;
+#pragma unroll
+    for (int dy = -1; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = -1; dx < 2; ++dx) {  // bmfr.cl:897-920
+            const int sx = x + dx, sy = y + dy;
+            if (sx >= 0 && sy >= 0 && sx < W && sy < H) {
+                f3 s = (dx == 0 && dy == 0) ? me : ld3(new_frame, (long)sy * W + sx);
+                s = rgb_to_ycocg(s);
+                if (dx == 0 || dy == 0) {
+                    mnc = f3{fminf(mnc.x, s.x), fminf(mnc.y, s.y), fminf(mnc.z, s.z)};
+                    mxc = f3{fmaxf(mxc.x, s.x), fmaxf(mxc.y, s.y), fmaxf(mxc.z, s.z)};
+                }
+                mnb = f3{fminf(mnb.x, s.x), fminf(mnb.y, s.y), fminf(mnb.z, s.z)};
+                mxb = f3{fmaxf(mxb.x, s.x), fmaxf(mxb.y, s.y), fmaxf(mxb.z, s.z)};
+            }
+        }
+    f3 prev{0.f, 0.f, 0.f};
+    float total = 0.f;
+    const float fx = pf.x - flx, fy = pf.y - fly;
+    const float omx = 1.f - fx, omy = 1.f - fy;
+    const float tw[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // bmfr.cl:929-960
+        const bool okx = (i & 1) ? (ix < W - 1) : (ix >= 0);
+        const bool oky = (i >> 1) ? (iy < H - 1) : (iy >= 0);
+        if (okx && oky) {
+            const f3 pc = ld3(prev_frame, (long)(iy + (i >> 1)) * W + ix + (i & 1));
+            prev.x = prev.x + tw[i] * pc.x;
+            prev.y = prev.y + tw[i] * pc.y;
+            prev.z = prev.z + tw[i] * pc.z;
+            total = total + tw[i];
+        }
+    }
+    prev = f3{prev.x / total, prev.y / total, prev.z / total};
+    const f3 py = rgb_to_ycocg(prev);
+    const f3 lo{(mnb.x + mnc.x) / 2.f, (mnb.y + mnc.y) / 2.f, (mnb.z + mnc.z) / 2.f};
+    const f3 hi{(mxb.x + mxc.x) / 2.f, (mxb.y + mxc.y) / 2.f, (mxb.z + mxc.z) / 2.f};
+    const f3 cl{fminf(fmaxf(py.x, lo.x), hi.x), fminf(fmaxf(py.y, lo.y), hi.y),
+                fminf(fmaxf(py.z, lo.z), hi.z)};
+    const f3 pr = ycocg_to_rgb(cl);
+    const float a = P.taa_blend_alpha, b = 1.f - a;
+    st3(result, lin, f3{a * me.x + b * pr.x, a * me.y + b * pr.y, a * me.z + b * pr.z});
+}
+
+// ------------------------------------------------------------ fused K1 ----
+template <int NS, int FS, bool HALF>
+__global__ __launch_bounds__(256) void k_fused_block(Params P, NoisyInputs in, Camera cam, int frame,
+                                                     const float* __restrict__ albedo,
+                                                     const float* __restrict__ acc_prev,
+                                                     float* __restrict__ noisy_out,
+                                                     uint8_t* __restrict__ spp_out,
+                                                     float2* __restrict__ prev_pixel_out,
+                                                     float* __restrict__ acc_out,
+                                                     float* __restrict__ tone_out) {
+    constexpr int B = NS + FS + 3;
+    __shared__ FitLds<B> L;
+    const int t = threadIdx.x, g = blockIdx.x;
+    const int bx = g % P.blocks_x, by = g / P.blocks_x;
+
+    float a[B][kSubs];
+    f3 n_keep[kSubs], p_keep[kSubs];
+    float pfx[kSubs], pfy[kSubs];
+    long lin[kSubs];
+    uint32_t flags = 0;  // per s: bit 8s owner, bits 8s+1.. accept(4)
+    uint32_t spps = 0;
+#pragma unroll
+    for (int s = 0; s < kSubs; ++s) {
+        const int r = t + s * kLocal;
+        const int gx = bx * kEdge + (r & (kEdge - 1)), gy = by * kEdge + (r >> 5);
+        const NoisyItem it = noisy_item(P, in, cam, gx, gy, frame);
+#pragma unroll
+        for (int f = 0; f < B; ++f) {
+            const float v = design_value(P, f, it);
+            a[f][s] = HALF ? round_half(v) : v;
+        }
+        n_keep[s] = it.n;
+        p_keep[s] = it.p;
+        pfx[s] = it.pfx;
+        pfy[s] = it.pfy;
+        lin[s] = it.lin;
+        flags |= ((uint32_t)it.owner | ((uint32_t)it.accept << 1)) << (8 * s);
+        spps |= (uint32_t)it.spp << (8 * s);
+        if (it.owner) {
+            st3(noisy_out, it.lin, it.color);
+            spp_out[it.lin] = it.spp;
+            prev_pixel_out[it.lin] = make_float2(it.pfx, it.pfy);
+        }
+    }
+
+    fit_block<NS, FS, HALF, false, true>(a, L, t, frame, P.noise2);
+
+#pragma unroll
+    for (int s = 0; s < kSubs; ++s) {
+        const uint32_t fl = flags >> (8 * s);
+        if (fl & 1u) {
+            const f3 filtered = weighted_color(P, L.weights, L.minmax, n_keep[s], p_keep[s]);
+            f3 tone;
+            const f3 acc = accumulate_filtered(P, filtered, pfx[s], pfy[s], (uint8_t)((fl >> 1) & 15u),
+                                               (uint8_t)(spps >> (8 * s)), ld3(albedo, lin[s]),
+                                               acc_prev, frame, &tone);
+            st3(acc_out, lin[s], acc);
+            st3(tone_out, lin[s], tone);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- launch --
+namespace {
+dim3 grid2d(int w, int h, dim3 blk) { return dim3((w + blk.x - 1) / blk.x, (h + blk.y - 1) / blk.y); }
+}  // namespace
+
+hipError_t launch_accumulate_noisy(const Params& P, hipStream_t st, float2* prev_pixel, uint8_t* accept,
+                                   const NoisyInputs& in, float* noisy_out, uint8_t* spp_cur, void* tmp,
+                                   const Camera& cam, int frame) {
+    const dim3 blk(16, 16);
+    const dim3 grd = grid2d(P.margins_w, P.margins_h, blk);
+    for (int pass = 0; pass < 2; ++pass) {
+        hipLaunchKernelGGL(k_accumulate_noisy, grd, blk, 0, st, P, in, cam, frame, pass, prev_pixel,
+                           accept, noisy_out, spp_cur, tmp);
+    }
+    return hipGetLastError();
+}
+
+template <int NS, int FS>
+static hipError_t launch_fitter_t(const Params& P, hipStream_t st, float* w, float* mm, void* tmp,
+                                  int frame) {
+    const int G = P.blocks_x * P.blocks_y;
+    if (P.half_tmp) hipLaunchKernelGGL((k_fitter<NS, FS, true>), dim3(G), dim3(256), 0, st, P, w, mm, tmp, frame);
+    else hipLaunchKernelGGL((k_fitter<NS, FS, false>), dim3(G), dim3(256), 0, st, P, w, mm, tmp, frame);
+    return hipGetLastError();
+}
+
+bool fitter_supported(int ns, int fs) { return ns == 4 && (fs == 6 || fs == 9); }
+
+hipError_t launch_fitter(const Params& P, hipStream_t st, float* weights, float* mins_maxs, void* tmp,
+                         int frame) {
+    if (P.not_scaled == 4 && P.scaled == 6) return launch_fitter_t<4, 6>(P, st, weights, mins_maxs, tmp, frame);
+    if (P.not_scaled == 4 && P.scaled == 9) return launch_fitter_t<4, 9>(P, st, weights, mins_maxs, tmp, frame);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_weighted_sum(const Params& P, hipStream_t st, const float* weights,
+                               const float* mins_maxs, float* out, const float* normals,
+                               const float* positions, int frame) {
+    const dim3 blk(64, 4);
+    hipLaunchKernelGGL(k_weighted_sum, grid2d(P.width, P.height, blk), blk, 0, st, P, weights,
+                       mins_maxs, out, normals, positions, frame);
+    return hipGetLastError();
+}
+
+hipError_t launch_accumulate_filtered(const Params& P, hipStream_t st, const float* filtered,
+                                      const float2* prev_pixel, const uint8_t* accept,
+                                      const float* albedo, float* tone, const uint8_t* spp,
+                                      const float* acc_prev, float* acc, int frame) {
+    const dim3 blk(64, 4);
+    hipLaunchKernelGGL(k_accumulate_filtered, grid2d(P.width, P.height, blk), blk, 0, st, P, filtered,
+                       prev_pixel, accept, albedo, tone, spp, acc_prev, acc, frame);
+    return hipGetLastError();
+}
+
+hipError_t launch_taa(const Params& P, hipStream_t st, const float2* prev_pixel, const float* new_frame,
+                      float* result, const float* prev_frame, int frame) {
+    const dim3 blk(64, 4);
+    hipLaunchKernelGGL(k_taa, grid2d(P.width, P.height, blk), blk, 0, st, P, prev_pixel, new_frame,
+                       result, prev_frame, frame);
+    return hipGetLastError();
+}
+
+template <int NS, int FS>
+static hipError_t launch_fused_t(const Params& P, hipStream_t st, const FusedArgs& A) {
+    const int G = P.blocks_x * P.blocks_y;
+    if (P.half_tmp)
+        hipLaunchKernelGGL((k_fused_block<NS, FS, true>), dim3(G), dim3(256), 0, st, P, A.in, A.cam,
+                           A.frame, A.albedo, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out,
+                           A.acc_out, A.tone_out);
+    else
+        hipLaunchKernelGGL((k_fused_block<NS, FS, false>), dim3(G), dim3(256), 0, st, P, A.in, A.cam,
+                           A.frame, A.albedo, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out,
+                           A.acc_out, A.tone_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& A, hipEvent_t mid) {
+    hipError_t e;
+    if (P.not_scaled == 4 && P.scaled == 6) e = launch_fused_t<4, 6>(P, st, A);
+    else if (P.not_scaled == 4 && P.scaled == 9) e = launch_fused_t<4, 9>(P, st, A);
+    else return hipErrorInvalidValue;
+    if (e != hipSuccess) return e;
+    if (mid) (void)hipEventRecord(mid, st);
+    return launch_taa(P, st, A.prev_pixel_out, A.tone_out, A.result_out, A.result_prev, A.frame);
+}
+
+}  // namespace bmfr

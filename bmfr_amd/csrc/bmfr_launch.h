@@ -1,0 +1,44 @@
+// bmfr_launch.h -- host-side launchers of bmfr_kernels.hip (used by the C ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "bmfr_kernels.h"
+
+namespace bmfr {
+
+// Arguments of one fused frame (K1 + K2).
+struct FusedArgs {
+    NoisyInputs in;
+    Camera cam;
+    int frame;
+    const float* albedo;
+    const float* acc_prev;
+    const float* result_prev;
+    float* noisy_out;
+    uint8_t* spp_out;
+    float2* prev_pixel_out;
+    float* acc_out;
+    float* tone_out;
+    float* result_out;
+};
+
+bool fitter_supported(int not_scaled, int scaled);
+
+hipError_t launch_accumulate_noisy(const Params& P, hipStream_t st, float2* prev_pixel, uint8_t* accept,
+                                   const NoisyInputs& in, float* noisy_out, uint8_t* spp_cur, void* tmp,
+                                   const Camera& cam, int frame);
+hipError_t launch_fitter(const Params& P, hipStream_t st, float* weights, float* mins_maxs, void* tmp,
+                         int frame);
+hipError_t launch_weighted_sum(const Params& P, hipStream_t st, const float* weights,
+                               const float* mins_maxs, float* out, const float* normals,
+                               const float* positions, int frame);
+hipError_t launch_accumulate_filtered(const Params& P, hipStream_t st, const float* filtered,
+                                      const float2* prev_pixel, const uint8_t* accept,
+                                      const float* albedo, float* tone, const uint8_t* spp,
+                                      const float* acc_prev, float* acc, int frame);
+hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& A, hipEvent_t mid = nullptr);
+hipError_t launch_taa(const Params& P, hipStream_t st, const float2* prev_pixel, const float* new_frame,
+                      float* result, const float* prev_frame, int frame);
+
+}  // namespace bmfr

@@ -1,0 +1,283 @@
+"""Host-side mirror of the reference's frame driver over libbmfr's C ABI.
+
+Reference: tasks() in /root/reference/opencl/bmfr.cpp:179-556.
+
+* `BmfrConfig` is the `#define` surface of bmfr.cpp:32-118.
+* `StagePipeline` replays tasks()' frame loop (bmfr.cpp:417-485) one stage at
+  a time on torch-owned device buffers laid out like the reference's
+  cl::Buffers (bmfr.cpp:315-347), including the Double_buffer swap
+  (bmfr.cpp:122-135, 482-484).  It exists so every intermediate buffer can be
+  compared with the reference kernels and the CPU oracle.
+* `Denoiser` is the production path: one `bmfr_process_frame` per frame
+  (fused K1 + TAA), temporal state owned by the C context.
+
+Device memory, streams and copies come from torch; the compute is libbmfr's
+HIP kernels.  Nothing here falls back to a CPU implementation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+
+import torch
+
+from . import _lib
+from ._lib import check, floats
+
+NOT_SCALED_DEFAULT = (_lib.FEATURE_ONE, _lib.NORMAL_X, _lib.NORMAL_Y, _lib.NORMAL_Z)
+SCALED_DEFAULT = (_lib.POSITION_X, _lib.POSITION_Y, _lib.POSITION_Z,
+                  _lib.POSITION_X2, _lib.POSITION_Y2, _lib.POSITION_Z2)
+SCALED_THIRD_ORDER = SCALED_DEFAULT + (_lib.POSITION_X3, _lib.POSITION_Y3, _lib.POSITION_Z3)
+
+
+@dataclasses.dataclass(frozen=True)
+class BmfrConfig:
+    """bmfr.cpp's compile-time parameters (names follow the #defines)."""
+    image_width: int = 1280                  # IMAGE_WIDTH  bmfr.cpp:39
+    image_height: int = 720                  # IMAGE_HEIGHT bmfr.cpp:40
+    not_scaled: tuple = NOT_SCALED_DEFAULT   # NOT_SCALED_FEATURE_BUFFERS bmfr.cpp:65-69
+    scaled: tuple = SCALED_DEFAULT           # SCALED_FEATURE_BUFFERS bmfr.cpp:71-77
+    noise_amount: float = 1e-2               # NOISE_AMOUNT bmfr.cpp:58
+    blend_alpha: float = 0.2                 # BLEND_ALPHA bmfr.cpp:60
+    second_blend_alpha: float = 0.1          # SECOND_BLEND_ALPHA bmfr.cpp:61
+    taa_blend_alpha: float = 0.2             # TAA_BLEND_ALPHA bmfr.cpp:62
+    position_limit_squared: float = 0.01     # camera_matrices.h, bmfr.cpp:226
+    normal_limit_squared: float = 0.1        # camera_matrices.h, bmfr.cpp:227
+    use_half_precision_in_tmp_data: int = 1  # bmfr.cpp:88
+
+    @property
+    def buffer_count(self) -> int:
+        return len(self.not_scaled) + len(self.scaled) + 3
+
+    def to_c(self) -> _lib.Config:
+        lib = _lib.load()
+        c = _lib.Config()
+        lib.bmfr_config_default(C.byref(c), self.image_width, self.image_height)
+        feats = tuple(self.not_scaled) + tuple(self.scaled)
+        c.features_not_scaled = len(self.not_scaled)
+        c.features_scaled = len(self.scaled)
+        for i in range(_lib.MAX_FEATURES):
+            c.feature_buffers[i] = feats[i] if i < len(feats) else 0
+        c.noise_amount = self.noise_amount
+        c.blend_alpha = self.blend_alpha
+        c.second_blend_alpha = self.second_blend_alpha
+        c.taa_blend_alpha = self.taa_blend_alpha
+        c.position_limit_squared = self.position_limit_squared
+        c.normal_limit_squared = self.normal_limit_squared
+        c.use_half_precision_in_tmp_data = self.use_half_precision_in_tmp_data
+        return c
+
+    def sizes(self) -> _lib.Sizes:
+        s = _lib.Sizes()
+        check(_lib.load().bmfr_config_sizes(C.byref(self.to_c()), C.byref(s)), "bmfr_config_sizes")
+        return s
+
+
+def _ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(stream) -> int | None:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+class _Context:
+    def __init__(self, cfg: BmfrConfig, device: int = 0):
+        self.cfg = cfg
+        self.lib = _lib.load()
+        self.device = device
+        h = C.c_void_p()
+        check(self.lib.bmfr_create(C.byref(cfg.to_c()), device, C.byref(h)), "bmfr_create")
+        self.handle = h
+        self.sizes = cfg.sizes()
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.bmfr_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class StagePipeline(_Context):
+    """The reference frame loop, stage by stage, on reference-layout buffers."""
+
+    def __init__(self, cfg: BmfrConfig, device: int = 0):
+        super().__init__(cfg, device)
+        dev = torch.device("cuda", device)
+        W, H = cfg.image_width, cfg.image_height
+        s = self.sizes
+        f32 = dict(dtype=torch.float32, device=dev)
+        img = lambda: torch.zeros(H * W * 3, **f32)  # noqa: E731
+        self.normals = [img(), img()]
+        self.positions = [img(), img()]
+        self.noisy = [img(), img()]
+        self.out = [img(), img()]          # accumulated filtered colour
+        self.result = [img(), img()]       # TAA output
+        self.spp = [torch.zeros(H * W, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.albedo = img()
+        self.filtered = img()
+        self.tone_mapped = img()
+        self.prev_pixels = torch.zeros(H * W * 2, **f32)
+        self.accept = torch.zeros(H * W, dtype=torch.uint8, device=dev)
+        tmp_elems = s.tmp_data_bytes // (2 if cfg.use_half_precision_in_tmp_data else 4)
+        self.tmp_data = torch.zeros(tmp_elems, dtype=torch.float16 if cfg.use_half_precision_in_tmp_data
+                                    else torch.float32, device=dev)
+        self.weights = torch.zeros(s.weights_bytes // 4, **f32)
+        self.mins_maxs = torch.zeros(s.mins_maxs_bytes // 4, **f32)
+        self.swapped = False
+
+    def cur(self, pair):
+        return pair[0] if self.swapped else pair[1]   # Double_buffer::current, bmfr.cpp:132
+
+    def prev(self, pair):
+        return pair[1] if self.swapped else pair[0]   # Double_buffer::previous, bmfr.cpp:133
+
+    def upload(self, noisy, normals, positions, albedo) -> None:
+        """enqueueWriteBuffer of bmfr.cpp:420-427 (device-to-device here)."""
+        self.cur(self.noisy).copy_(noisy.reshape(-1))
+        self.cur(self.normals).copy_(normals.reshape(-1))
+        self.cur(self.positions).copy_(positions.reshape(-1))
+        self.albedo.copy_(albedo.reshape(-1))
+
+    def run_stages(self, prev_vp, jitter, frame: int, stream=None, record=None) -> None:
+        lib, h, st = self.lib, self.handle, _stream(stream)
+        vp, jt = floats(prev_vp, 16), floats(jitter, 2)
+        check(lib.bmfr_accumulate_noisy_data(
+            h, st, _ptr(self.prev_pixels), _ptr(self.accept), _ptr(self.cur(self.normals)),
+            _ptr(self.prev(self.normals)), _ptr(self.cur(self.positions)), _ptr(self.prev(self.positions)),
+            _ptr(self.cur(self.noisy)), _ptr(self.prev(self.noisy)), _ptr(self.prev(self.spp)),
+            _ptr(self.cur(self.spp)), _ptr(self.tmp_data), vp, jt, frame), "accumulate_noisy_data")
+        if record is not None:
+            record["tmp_noisy"] = self.tmp_data.clone()
+        check(lib.bmfr_fitter(h, st, _ptr(self.weights), _ptr(self.mins_maxs), _ptr(self.tmp_data), frame),
+              "fitter")
+        check(lib.bmfr_weighted_sum(h, st, _ptr(self.weights), _ptr(self.mins_maxs), _ptr(self.filtered),
+                                    _ptr(self.cur(self.normals)), _ptr(self.cur(self.positions)),
+                                    _ptr(self.cur(self.noisy)), frame), "weighted_sum")
+        check(lib.bmfr_accumulate_filtered_data(
+            h, st, _ptr(self.filtered), _ptr(self.prev_pixels), _ptr(self.accept), _ptr(self.albedo),
+            _ptr(self.tone_mapped), _ptr(self.cur(self.spp)), _ptr(self.prev(self.out)),
+            _ptr(self.cur(self.out)), frame), "accumulate_filtered_data")
+        check(lib.bmfr_taa(h, st, _ptr(self.prev_pixels), _ptr(self.tone_mapped),
+                           _ptr(self.cur(self.result)), _ptr(self.prev(self.result)), frame), "taa")
+        if record is not None:
+            record.update(
+                tmp_fit=self.tmp_data.clone(), weights=self.weights.clone(),
+                mins_maxs=self.mins_maxs.clone(), filtered=self.filtered.clone(),
+                acc=self.cur(self.out).clone(), tone=self.tone_mapped.clone(),
+                result=self.cur(self.result).clone(), spp=self.cur(self.spp).clone(),
+                accept=self.accept.clone(), prev_pixel=self.prev_pixels.clone(),
+                noisy=self.cur(self.noisy).clone())
+
+    def swap(self) -> None:
+        self.swapped = not self.swapped             # bmfr.cpp:482-484
+
+
+class Denoiser(_Context):
+    """Production path: one fused `bmfr_process_frame` per frame."""
+
+    def __init__(self, cfg: BmfrConfig, device: int = 0):
+        super().__init__(cfg, device)
+        self.prev_inputs = None
+
+    def process_frame(self, noisy, normals, positions, albedo, prev_vp, jitter, frame: int,
+                      prev_normals=None, prev_positions=None, stream=None) -> None:
+        """Run one frame.  prev_normals / prev_positions default to the ones
+        passed on the previous call (the reference's Double_buffer halves)."""
+        if frame > 0 and prev_normals is None:
+            if self.prev_inputs is None:
+                raise ValueError("frame > 0 needs the previous frame's normals/positions")
+            prev_normals, prev_positions = self.prev_inputs
+        fi = _lib.FrameInputs(_ptr(noisy), _ptr(normals), _ptr(positions), _ptr(albedo),
+                              _ptr(prev_normals), _ptr(prev_positions))
+        check(self.lib.bmfr_process_frame(self.handle, _stream(stream), C.byref(fi), floats(prev_vp, 16),
+                                          floats(jitter, 2), frame), "bmfr_process_frame")
+        self.prev_inputs = (normals, positions)
+
+    def set_profiling(self, enable: bool, capacity: int = 4096) -> None:
+        check(self.lib.bmfr_set_profiling(self.handle, int(enable), capacity), "bmfr_set_profiling")
+
+    def profile(self):
+        """Per-frame device timings [(frame, k1_ms, taa_ms, total_ms)] since profiling was enabled."""
+        n = C.c_int()
+        check(self.lib.bmfr_get_profile(self.handle, None, 0, C.byref(n)), "bmfr_get_profile")
+        buf = (_lib.FrameProfile * 65536)()
+        check(self.lib.bmfr_get_profile(self.handle, buf, 65536, C.byref(n)), "bmfr_get_profile")
+        return [(p.frame_number, p.fused_block_ms, p.taa_ms, p.total_ms) for p in buf[:n.value]]
+
+    def state(self, previous: bool = False) -> _lib.StateView:
+        v = _lib.StateView()
+        check(self.lib.bmfr_state(self.handle, int(previous), C.byref(v)), "bmfr_state")
+        return v
+
+    def output_ptr(self) -> int:
+        p = self.lib.bmfr_output(self.handle)
+        if not p:
+            raise RuntimeError("no frame processed yet")
+        return p
+
+    def copy_output(self, dst: torch.Tensor, stream=None) -> torch.Tensor:
+        """Copy the last frame's TAA output (float3, W*H) into `dst`."""
+        hip_memcpy_d2d(dst.data_ptr(), self.output_ptr(), self.sizes.image_bytes, stream)
+        return dst
+
+    def copy_state(self, name: str, dst: torch.Tensor, previous: bool = False, stream=None) -> torch.Tensor:
+        ptr = getattr(self.state(previous), name)
+        hip_memcpy_d2d(dst.data_ptr(), ptr, dst.numel() * dst.element_size(), stream)
+        return dst
+
+
+_hip = None
+
+
+def hip_memcpy_d2d(dst: int, src: int, nbytes: int, stream=None) -> None:
+    """hipMemcpyAsync device-to-device on the torch stream (torch's HIP runtime)."""
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so.7")
+        _hip.hipMemcpyAsync.restype = C.c_int
+        _hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+    err = _hip.hipMemcpyAsync(dst, src, nbytes, 3, _stream(stream))  # 3 = hipMemcpyDeviceToDevice
+    if err != 0:
+        raise RuntimeError(f"hipMemcpyAsync failed: {err}")
+
+
+def synth_camera(width: int, height: int, frame: int):
+    """(column-major VP of `frame`, pixel offset of `frame`) of the synthetic sequence."""
+    vp = (C.c_float * 16)()
+    off = (C.c_float * 2)()
+    _lib.load().bmfr_synth_camera(width, height, frame, vp, off)
+    return list(vp), list(off)
+
+
+def synth_frame_host(width: int, height: int, frame: int, seed: int = 0x424D4652, clean: bool = False):
+    """Render synthetic frame `frame` on the CPU -> dict of float32 numpy (H, W, 3)."""
+    import numpy as np
+    out = {k: np.empty((height, width, 3), np.float32) for k in ("noisy", "normals", "positions", "albedo")}
+    if clean:
+        out["clean"] = np.empty((height, width, 3), np.float32)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    check(_lib.load().bmfr_synth_frame_host(width, height, frame, seed, p(out["noisy"]), p(out["normals"]),
+                                            p(out["positions"]), p(out["albedo"]),
+                                            p(out["clean"]) if clean else None), "bmfr_synth_frame_host")
+    return out
+
+
+def synth_frame_device(width: int, height: int, frame: int, seed: int = 0x424D4652, device: int = 0,
+                       clean: bool = False, out=None, stream=None):
+    """Render synthetic frame `frame` on the GPU -> dict of float32 tensors (H*W*3)."""
+    dev = torch.device("cuda", device)
+    keys = ("noisy", "normals", "positions", "albedo") + (("clean",) if clean else ())
+    if out is None:
+        out = {k: torch.empty(height * width * 3, dtype=torch.float32, device=dev) for k in keys}
+    check(_lib.load().bmfr_synth_frame_device(width, height, frame, seed, _ptr(out["noisy"]),
+                                              _ptr(out["normals"]), _ptr(out["positions"]),
+                                              _ptr(out["albedo"]), _ptr(out.get("clean")),
+                                              _stream(stream)), "bmfr_synth_frame_device")
+    return out

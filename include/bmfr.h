@@ -1,0 +1,223 @@
+/* bmfr.h -- C ABI of libbmfr, the MI355X-native BMFR denoiser.
+ *
+ * This is the drop-in boundary for the reference's hot path, the per-frame
+ * pipeline of /root/reference/opencl/bmfr.cl driven by tasks() in
+ * /root/reference/opencl/bmfr.cpp.  The reference has no plugin API: its
+ * boundary is (a) the JIT `-D` option set of bmfr.cpp:205-232, mirrored here
+ * by bmfr_config, and (b) the five OpenCL kernel signatures with the argument
+ * binding of bmfr.cpp:349-383,429-476, mirrored by the five stage entry
+ * points below with the same argument roles and buffer layouts.  On top,
+ * bmfr_process_frame runs one whole frame (the loop body of
+ * bmfr.cpp:417-485) through the fused MI355X kernels.
+ *
+ * Conventions
+ *  - Plain C: pointers, sizes and a status code.  No exceptions cross the ABI
+ *    (the reference maps cl::Error to a return code, bmfr.cpp:558-578).
+ *  - All buffer pointers are device pointers (hipMalloc / torch tensors).
+ *  - `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ *  - Layouts (bmfr.cpp:315-347): float3 images are interleaved RGB f32 with
+ *    row stride image_width; u8 planes (spp, accept) and float2 prev-pixel
+ *    planes likewise; tmp_data is [block][feature][32*32] (bmfr.cl:455-464)
+ *    in IEEE half (use_half_precision_in_tmp_data = 1) or f32; weights are
+ *    [block][B-3][3] f32; mins_maxs are [block][FEATURES_SCALED][2] f32.
+ *  - A context is not thread-safe; contexts are independent (one per GPU).
+ */
+#ifndef BMFR_H
+#define BMFR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BMFR_VERSION_MAJOR 0
+#define BMFR_VERSION_MINOR 1
+
+#define BMFR_BLOCK_EDGE_LENGTH 32 /* bmfr.cpp:104; other sizes unsupported, as upstream */
+#define BMFR_MAX_FEATURES 16      /* NOT_SCALED + SCALED feature buffers */
+
+typedef enum bmfr_status {
+    BMFR_OK = 0,
+    BMFR_ERROR_INVALID_ARGUMENT = 1,
+    BMFR_ERROR_UNSUPPORTED = 2,     /* e.g. a feature count with no compiled kernel */
+    BMFR_ERROR_OUT_OF_MEMORY = 3,
+    BMFR_ERROR_HIP = 4,             /* a HIP runtime call failed (see bmfr_last_hip_error) */
+    BMFR_ERROR_NO_DEVICE = 5
+} bmfr_status;
+
+/* Feature buffer monomials.  The reference pastes C expressions into the
+ * kernels (NOT_SCALED_FEATURE_BUFFERS / SCALED_FEATURE_BUFFERS, bmfr.cpp:65-77
+ * -> FEATURE_BUFFERS, bmfr.cl:448-453,727-729); this ABI names them. */
+typedef enum bmfr_feature {
+    BMFR_FEATURE_ONE = 0, /* "1.f" */
+    BMFR_FEATURE_NORMAL_X, BMFR_FEATURE_NORMAL_Y, BMFR_FEATURE_NORMAL_Z,
+    BMFR_FEATURE_POSITION_X, BMFR_FEATURE_POSITION_Y, BMFR_FEATURE_POSITION_Z,
+    BMFR_FEATURE_POSITION_X2, BMFR_FEATURE_POSITION_Y2, BMFR_FEATURE_POSITION_Z2,
+    BMFR_FEATURE_POSITION_X3, BMFR_FEATURE_POSITION_Y3, BMFR_FEATURE_POSITION_Z3,
+    BMFR_FEATURE_COUNT_
+} bmfr_feature;
+
+/* The reference's #define surface (bmfr.cpp:32-118, forwarded as -D at
+ * bmfr.cpp:205-232).  Fill with bmfr_config_default() and override. */
+typedef struct bmfr_config {
+    int image_width;                     /* IMAGE_WIDTH  (bmfr.cpp:39) */
+    int image_height;                    /* IMAGE_HEIGHT (bmfr.cpp:40) */
+    int features_not_scaled;             /* FEATURES_NOT_SCALED (bmfr.cpp:195-196) */
+    int features_scaled;                 /* FEATURES_SCALED     (bmfr.cpp:198-199) */
+    int feature_buffers[BMFR_MAX_FEATURES]; /* FEATURE_BUFFERS: not-scaled then scaled */
+    double noise_amount;                 /* NOISE_AMOUNT 1e-2 (a double, bmfr.cpp:58) */
+    float blend_alpha;                   /* BLEND_ALPHA 0.2f        (bmfr.cpp:60) */
+    float second_blend_alpha;            /* SECOND_BLEND_ALPHA 0.1f (bmfr.cpp:61) */
+    float taa_blend_alpha;               /* TAA_BLEND_ALPHA 0.2f    (bmfr.cpp:62) */
+    double position_limit_squared;       /* camera_matrices.h value; used as the
+                                            kernel sees it: float(%g text), bmfr.cpp:226 */
+    double normal_limit_squared;         /* idem, bmfr.cpp:227 */
+    int use_half_precision_in_tmp_data;  /* USE_HALF_PRECISION_IN_TMP_DATA 1 (bmfr.cpp:88) */
+    /* Spatial tile of a larger frame (multi-GPU sharding); 0/0/0/0 = whole
+     * image.  Tiles use the global block grid and global image borders. */
+    int tile_x, tile_y, tile_width, tile_height;
+} bmfr_config;
+
+/* Sizes derived from a config (bmfr.cpp:104-118, 316-343). */
+typedef struct bmfr_sizes {
+    int buffer_count;       /* BUFFER_COUNT = not_scaled + scaled + 3 */
+    int r_edge;             /* R_EDGE = BUFFER_COUNT - 2 */
+    int workset_width, workset_height;                           /* WORKSET_* */
+    int workset_with_margins_width, workset_with_margins_height; /* WORKSET_WITH_MARGINS_* */
+    int blocks;             /* fitter work-groups, FITTER_GLOBAL / 256 */
+    size_t tmp_data_bytes;  /* in_buffer, bmfr.cpp:322-324 */
+    size_t weights_bytes;   /* bmfr.cpp:338-339 */
+    size_t mins_maxs_bytes; /* sized from FEATURES_SCALED (bmfr.cpp:340 assumes 6) */
+    size_t image_bytes;     /* one float3 plane, W*H*3*4 */
+} bmfr_sizes;
+
+typedef struct bmfr_ctx bmfr_ctx;
+
+void bmfr_config_default(bmfr_config *cfg, int image_width, int image_height);
+bmfr_status bmfr_config_sizes(const bmfr_config *cfg, bmfr_sizes *out);
+const char *bmfr_status_string(bmfr_status s);
+int bmfr_last_hip_error(void);
+
+/* Replaces clutils::CLEnv + the addContext/addQueue/addProgram calls
+ * (bmfr.cpp:183-243): binds a HIP device and selects the kernels. */
+bmfr_status bmfr_create(const bmfr_config *cfg, int hip_device, bmfr_ctx **out);
+bmfr_status bmfr_destroy(bmfr_ctx *ctx);
+bmfr_status bmfr_get_sizes(const bmfr_ctx *ctx, bmfr_sizes *out);
+
+/* ---- Stage API: one entry per reference kernel, same argument roles ---- */
+
+/* accumulate_noisy_data, bmfr.cl:290-308 (args bound at bmfr.cpp:351-352,429-447).
+ * current_noisy is in/out like the reference.  Margin work-items read the
+ * colours current_noisy held before the call (race-free form of
+ * bmfr.cl:316-322 vs 478-481). */
+bmfr_status bmfr_accumulate_noisy_data(bmfr_ctx *ctx, void *stream,
+    float *out_prev_frame_pixel, uint8_t *accept_bools,
+    const float *current_normals, const float *previous_normals,
+    const float *current_positions, const float *previous_positions,
+    float *current_noisy, const float *previous_noisy,
+    const uint8_t *previous_spp, uint8_t *current_spp, void *tmp_data,
+    const float prev_frame_camera_matrix[16], const float pixel_offset[2],
+    int frame_number);
+
+/* fitter, bmfr.cl:490-501 (args bound at bmfr.cpp:363-367,449-453).  The LDS
+ * scratch arguments of the OpenCL kernel are internal here. */
+bmfr_status bmfr_fitter(bmfr_ctx *ctx, void *stream, float *weights, float *mins_maxs,
+    void *tmp_data, int frame_number);
+
+/* weighted_sum, bmfr.cl:703-710 (bmfr.cpp:370-372,455-461).  current_noisy is
+ * accepted for signature parity; the reference uses it only for debugging. */
+bmfr_status bmfr_weighted_sum(bmfr_ctx *ctx, void *stream, const float *weights,
+    const float *mins_maxs, float *output, const float *current_normals,
+    const float *current_positions, const float *current_noisy, int frame_number);
+
+/* accumulate_filtered_data, bmfr.cl:761-770 (bmfr.cpp:375-379,463-469). */
+bmfr_status bmfr_accumulate_filtered_data(bmfr_ctx *ctx, void *stream,
+    const float *filtered_frame, const float *in_prev_frame_pixel,
+    const uint8_t *accept_bools, const float *albedo, float *tone_mapped_frame,
+    const uint8_t *current_spp, const float *accumulated_prev_frame,
+    float *accumulated_frame, int frame_number);
+
+/* taa, bmfr.cl:860-865 (bmfr.cpp:382-383,471-476). */
+bmfr_status bmfr_taa(bmfr_ctx *ctx, void *stream, const float *in_prev_frame_pixel,
+    const float *new_frame, float *result_frame, const float *prev_frame,
+    int frame_number);
+
+/* ---- Frame API: the loop body of bmfr.cpp:417-485 on fused kernels ---- */
+
+/* One frame's inputs (the four planes uploaded at bmfr.cpp:420-427) plus the
+ * previous frame's normals/positions (the Double_buffer halves the reference
+ * keeps, bmfr.cpp:316-319).  Temporal state (accumulated noisy colour, spp,
+ * accumulated filtered colour, TAA output) lives in the context and is
+ * double-buffered and swapped per frame like bmfr.cpp:482-484. */
+typedef struct bmfr_frame_inputs {
+    const float *noisy;           /* 1-spp colour (demodulated), float3 */
+    const float *normals;         /* shading normals, float3 */
+    const float *positions;       /* world positions, float3 */
+    const float *albedo;          /* float3 */
+    const float *prev_normals;    /* previous frame's normals (ignored at frame 0) */
+    const float *prev_positions;  /* previous frame's positions (ignored at frame 0) */
+} bmfr_frame_inputs;
+
+/* prev_frame_camera_matrix: column-major view-projection of frame-1
+ * (camera_matrices[max(frame-1,0)], bmfr.cpp:440-442); pixel_offset: the
+ * frame's jitter (pixel_offsets[frame], bmfr.cpp:443-444).  frame_number 0
+ * starts a new sequence. */
+bmfr_status bmfr_process_frame(bmfr_ctx *ctx, void *stream, const bmfr_frame_inputs *in,
+    const float prev_frame_camera_matrix[16], const float pixel_offset[2], int frame_number);
+
+/* Device pointer to the last processed frame's output (TAA result, float3,
+ * W*H, the buffer the reference reads back at bmfr.cpp:479-480).  Valid until
+ * the next bmfr_process_frame. */
+const float *bmfr_output(const bmfr_ctx *ctx);
+
+/* Device pointers to the context's temporal state of the last frame, for
+ * inspection / multi-GPU halo exchange: accumulated noisy colour (float3),
+ * spp (u8), accumulated filtered colour (float3), tone-mapped frame (float3),
+ * prev-frame pixel (float2), accept bits (u8). */
+typedef struct bmfr_state_view {
+    float *noisy_accumulated;
+    uint8_t *spp;
+    float *filtered_accumulated;
+    float *tone_mapped;
+    float *prev_frame_pixel;
+    uint8_t *accept;
+    float *result;
+} bmfr_state_view;
+bmfr_status bmfr_state(const bmfr_ctx *ctx, int previous, bmfr_state_view *out);
+
+/* ---- Profiling: the CL_QUEUE_PROFILING_ENABLE + GPUTimer analogue ----
+ * (bmfr.cpp:191, 386-412, 488-517).  When enabled, bmfr_process_frame records
+ * HIP events around its two kernels; bmfr_get_profile synchronises on them and
+ * returns per-frame device durations in ms, oldest first (at most `capacity`
+ * frames are kept; enabling again clears the record). */
+typedef struct bmfr_frame_profile {
+    int frame_number;
+    float fused_block_ms; /* K1: accumulate_noisy .. accumulate_filtered, fused */
+    float taa_ms;         /* K2: taa */
+    float total_ms;       /* start of K1 -> end of K2 (bmfr.cpp:497-502) */
+} bmfr_frame_profile;
+bmfr_status bmfr_set_profiling(bmfr_ctx *ctx, int enable, int capacity);
+bmfr_status bmfr_get_profile(bmfr_ctx *ctx, bmfr_frame_profile *out, int max_frames, int *count);
+
+/* ---- Synthetic scene (stands in for the external EXR dataset) ---- */
+
+/* Camera of frame `frame`: column-major view-projection matrix and the
+ * pixel offset (jitter) in [0,1)^2, i.e. camera_matrices[frame] and
+ * pixel_offsets[frame] of the dataset's camera_matrices.h (bmfr.cpp:44-53). */
+void bmfr_synth_camera(int image_width, int image_height, int frame, float vp[16],
+    float pixel_offset[2]);
+
+/* Render frame `frame` of the synthetic sequence into float3 planes.  `clean`
+ * (nullable) receives the noise-free tone-mapped reference image used for
+ * PSNR.  _host runs on the CPU (host pointers), _device on the GPU. */
+bmfr_status bmfr_synth_frame_host(int image_width, int image_height, int frame, uint32_t seed,
+    float *noisy, float *normals, float *positions, float *albedo, float *clean);
+bmfr_status bmfr_synth_frame_device(int image_width, int image_height, int frame, uint32_t seed,
+    float *noisy, float *normals, float *positions, float *albedo, float *clean, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BMFR_H */

@@ -1,0 +1,123 @@
+"""GPU parity tests (run on an MI355X: pytest -m gpu).
+
+Three implementations of the per-frame pipeline are compared frame by frame
+on the synthetic sequence, every inter-stage buffer recorded:
+
+  REF    the reference's own OpenCL kernels (/root/reference/opencl/bmfr.cl,
+         compiled by oracle/build_ref.py, launched through the HIP module API)
+  ORACLE the CPU restatement (oracle/bmfr_oracle.c)
+  HIP    libbmfr: the five stage kernels (StagePipeline) and the fused frame
+         path (Denoiser)
+
+Bars: HIP stages == REF(strict) bit for bit on every buffer; fused ==
+stages bit for bit; ORACLE == REF(strict) bit for bit except tone/result
+(powr: GPU library vs correctly rounded CPU pow, |diff| <= 2 ulp-ish); HIP
+vs REF(default build, contraction on) within relative L2 1e-4 (fp32 tmp)
+on the TAA output.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import bmfr_amd
+import pyoracle
+import ref_run
+from ref_configs import REF_CONFIGS
+from seq_util import (ALL_KEYS, EXACT_KEYS, POWR_KEYS, compare_exact, rel_l2, run_loop)
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = list(REF_CONFIGS)
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def bmfr_cfg(rc) -> bmfr_amd.BmfrConfig:
+    return bmfr_amd.BmfrConfig(image_width=rc.width, image_height=rc.height, not_scaled=rc.not_scaled,
+                               scaled=rc.scaled, use_half_precision_in_tmp_data=rc.half_tmp,
+                               position_limit_squared=rc.position_limit_squared,
+                               normal_limit_squared=rc.normal_limit_squared)
+
+
+_cache = {}
+
+
+def ref_frames(name, mode="strict"):
+    key = (name, mode)
+    if key not in _cache:
+        rc = REF_CONFIGS[name]
+        if not ref_run.available(name, mode):
+            pytest.skip(f"reference build {name}_{mode} missing (oracle/build_ref.py)")
+        _cache[key] = run_loop(ref_run.RefLoop(rc, mode), rc, rc.frames, to_device=_dev,
+                               sync=torch.cuda.synchronize)
+    return _cache[key]
+
+
+def stage_frames(name):
+    key = (name, "stages")
+    if key not in _cache:
+        rc = REF_CONFIGS[name]
+        _cache[key] = run_loop(bmfr_amd.StagePipeline(bmfr_cfg(rc)), rc, rc.frames, to_device=_dev,
+                               sync=torch.cuda.synchronize)
+    return _cache[key]
+
+
+@pytest.mark.parametrize("name", CONFIGS)
+def test_oracle_matches_reference_kernels(name, gpu):
+    """Pins the CPU oracle to the reference itself."""
+    rc = REF_CONFIGS[name]
+    ref = ref_frames(name)
+    cfg = pyoracle.make_cfg(rc.width, rc.height, rc.not_scaled, rc.scaled, rc.half_tmp)
+    orc = run_loop(pyoracle.OracleLoop(cfg), rc, rc.frames)
+    compare_exact(orc, ref, EXACT_KEYS, f"oracle vs reference[{name}]")
+    for f, (o, r) in enumerate(zip(orc, ref)):
+        for k in POWR_KEYS:
+            d = np.abs(o[k].astype(np.float64) - r[k])
+            assert d.max() <= 4e-7 * max(1.0, float(np.abs(r[k]).max())), (name, f, k, d.max())
+
+
+@pytest.mark.parametrize("name", CONFIGS)
+def test_stage_kernels_match_reference_bitwise(name, gpu):
+    compare_exact(stage_frames(name), ref_frames(name), ALL_KEYS, f"HIP stages vs reference[{name}]")
+
+
+@pytest.mark.parametrize("name", CONFIGS)
+def test_fused_frame_matches_stages_bitwise(name, gpu):
+    rc = REF_CONFIGS[name]
+    st = stage_frames(name)
+    den = bmfr_amd.Denoiser(bmfr_cfg(rc))
+    n = rc.width * rc.height
+    for f in range(rc.frames):
+        from seq_util import camera, frame_inputs
+        fr = {k: _dev(v) for k, v in frame_inputs(rc, f).items()}
+        vp, jit = camera(rc, f)
+        den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, f)
+        got = {
+            "result": den.copy_output(torch.empty(3 * n, device="cuda")),
+            "noisy": den.copy_state("noisy_accumulated", torch.empty(3 * n, device="cuda")),
+            "spp": den.copy_state("spp", torch.empty(n, dtype=torch.uint8, device="cuda")),
+            "acc": den.copy_state("filtered_accumulated", torch.empty(3 * n, device="cuda")),
+            "tone": den.copy_state("tone_mapped", torch.empty(3 * n, device="cuda")),
+            "prev_pixel": den.copy_state("prev_frame_pixel", torch.empty(2 * n, device="cuda")),
+        }
+        torch.cuda.synchronize()
+        for k, v in got.items():
+            a, b = v.cpu().numpy(), st[f][k]
+            assert a.tobytes() == b.tobytes(), (name, f, k, rel_l2(a, b) if a.dtype == np.float32 else
+                                                int((a != b).sum()))
+
+
+@pytest.mark.parametrize("name", CONFIGS)
+def test_against_reference_default_build(name, gpu):
+    """The reference as bmfr.cpp builds it (implementation-chosen contraction
+    and division); tolerance, since that build's rounding is not specified."""
+    rc = REF_CONFIGS[name]
+    ref = ref_frames(name, "default")
+    st = stage_frames(name)
+    worst = max(rel_l2(s["result"], r["result"]) for s, r in zip(st, ref))
+    print(f"{name}: worst per-frame rel-L2 vs default build = {worst:.3e}")
+    assert worst <= (1e-4 if not rc.half_tmp else 1e-3), worst
