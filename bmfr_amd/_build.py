@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libbmfr.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["bmfr_kernels.hip", "bmfr_capi.hip", "bmfr_synth.hip"]
+SOURCES = ["bmfr_kernels.hip", "bmfr_fused_wave.hip", "bmfr_capi.hip", "bmfr_synth.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-Wall", "-Wno-unused-function"]
 

@@ -26,6 +26,7 @@ struct bmfr_ctx {
     float* result[2] = {nullptr, nullptr};
     float* tone = nullptr;
     float2* prev_pixel = nullptr;
+    float* noise_table = nullptr;
     int cur = 0;
     bool has_frame = false;
     // Profiling ring: 3 events per frame (before K1, after K1, after K2).
@@ -99,6 +100,9 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     P.position_limit_sq = as_kernel_literal(c->position_limit_squared);
     P.normal_limit_sq = as_kernel_literal(c->normal_limit_squared);
     P.half_tmp = c->use_half_precision_in_tmp_data ? 1 : 0;
+    // Diagnostic override of the fused K1 kernel (A/B timing): BMFR_FUSED_KERNEL=block.
+    const char* v = std::getenv("BMFR_FUSED_KERNEL");
+    P.fused_variant = (v && std::strcmp(v, "block") == 0) ? 1 : 0;
     return P;
 }
 
@@ -199,6 +203,7 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
     }
     if (e == hipSuccess) e = hipMalloc(&c->tone, px * 3 * sizeof(float));
     if (e == hipSuccess) e = hipMalloc(&c->prev_pixel, px * sizeof(float2));
+    if (e == hipSuccess) e = hipMalloc(&c->noise_table, (size_t)bmfr::kMaxFeatures * bmfr::kBlockPixels * sizeof(float));
     if (e != hipSuccess) {
         bmfr_destroy(c);
         return hip_status(e);
@@ -221,6 +226,7 @@ bmfr_status bmfr_destroy(bmfr_ctx* c) {
     delete[] c->prof_frames;
     (void)hipFree(c->tone);
     (void)hipFree(c->prev_pixel);
+    (void)hipFree(c->noise_table);
     delete c;
     return BMFR_OK;
 }
@@ -330,6 +336,7 @@ bmfr_status bmfr_process_frame(bmfr_ctx* c, void* stream, const bmfr_frame_input
     A.acc_out = c->acc[cur];
     A.tone_out = c->tone;
     A.result_out = c->result[cur];
+    A.noise_table = c->noise_table;
     const bmfr_status st = hip_status(bmfr::launch_fused_frame(c->P, as_stream(stream), A, ev ? ev[1] : nullptr));
     if (st != BMFR_OK) return st;
     if (ev) {

@@ -25,13 +25,16 @@ struct f3 {
     float x, y, z;
 };
 
+// One float3 of an interleaved RGB plane as a single dwordx3 access.
+struct __attribute__((packed, aligned(4))) f3mem {
+    float x, y, z;
+};
 __device__ __forceinline__ f3 ld3(const float* __restrict__ b, long i) {
-    return f3{b[3 * i], b[3 * i + 1], b[3 * i + 2]};
+    const f3mem v = *reinterpret_cast<const f3mem*>(b + 3 * i);
+    return f3{v.x, v.y, v.z};
 }
 __device__ __forceinline__ void st3(float* __restrict__ b, long i, f3 v) {
-    b[3 * i] = v.x;
-    b[3 * i + 1] = v.y;
-    b[3 * i + 2] = v.z;
+    *reinterpret_cast<f3mem*>(b + 3 * i) = f3mem{v.x, v.y, v.z};
 }
 
 // OpenCL dot() as ROCm's opencl.bc implements it (fmuladd chain).
@@ -105,13 +108,24 @@ __device__ __forceinline__ f3 ycocg_to_rgb(f3 c) {
 extern "C" __device__ float __ocml_powr_f32(float, float);
 
 // Correctly rounded a / b given y = RN(1/b): one Markstein correction step
-// (r = a - q*b is exact under FMA; q + r*y rounds to RN(a/b) for normal
-// operands).  Used where one divisor serves many dividends (the fitter's
-// trailing update), in place of the ~10-instruction generic division.
+// (r = a - q*b is exact under FMA; q + r*y rounds to RN(a/b) when a, b, 1/b
+// and a/b are normal).  Used where one divisor serves several dividends, in
+// place of the ~10-instruction generic division.  Callers guarantee finite a
+// and finite, nonzero b with a normal reciprocal (see div_shared for the
+// guarded form).
 __device__ __forceinline__ float div_by_recip(float a, float b, float y) {
     const float q = a * y;
     const float r = __builtin_fmaf(-q, b, a);
     return __builtin_fmaf(r, y, q);
+}
+// Guarded form: where the correction step itself breaks down (a infinite,
+// b zero or infinite: r becomes NaN) the first quotient q = a * (1/b) already
+// is IEEE a / b, so use it.
+__device__ __forceinline__ float div_shared(float a, float b, float y) {
+    const float q = a * y;
+    const float r = __builtin_fmaf(-q, b, a);
+    const float q1 = __builtin_fmaf(r, y, q);
+    return q1 == q1 ? q1 : q;
 }
 
 }  // namespace bmfr

@@ -126,8 +126,9 @@ __device__ __forceinline__ NoisyItem noisy_item(const Params& P, const NoisyInpu
         float u = dot4(M[0], M[4], M[8], M[12], wp.x, wp.y, wp.z, 1.f);
         float v = dot4(M[1], M[5], M[9], M[13], wp.x, wp.y, wp.z, 1.f);
         const float w = dot4(M[3], M[7], M[11], M[15], wp.x, wp.y, wp.z, 1.f);
-        u = u / w;
-        v = v / w;
+        const float rw = 1.f / w;  // u / w and v / w share the divisor
+        u = div_shared(u, w, rw);
+        v = div_shared(v, w, rw);
         u = u + 1.f;
         v = v + 1.f;
         u = u / 2.f;
@@ -163,10 +164,11 @@ __device__ __forceinline__ NoisyItem noisy_item(const Params& P, const NoisyInpu
             }
         }
         if (total > 0.f) {  // bmfr.cl:421-429
-            prev.x = prev.x / total;
-            prev.y = prev.y / total;
-            prev.z = prev.z / total;
-            sample_spp = sample_spp / total;
+            const float rt = 1.f / total;
+            prev.x = div_shared(prev.x, total, rt);
+            prev.y = div_shared(prev.y, total, rt);
+            prev.z = div_shared(prev.z, total, rt);
+            sample_spp = div_shared(sample_spp, total, rt);
             alpha = 1.f / (sample_spp + 1.f);
             alpha = fmaxf(alpha, P.blend_alpha);
         }
@@ -384,5 +386,52 @@ __device__ __forceinline__ void fit_block(float (&a)[NS + FS + 3][kSubs], FitLds
     }
     __syncthreads();
 }
+
+// --------------------------------------------------------------------------
+// Temporal blend of the filtered colour, albedo remodulation and the
+// 1/2.2 gamma (bmfr.cl:761-857).  Returns the accumulated colour; *tone gets
+// the tone-mapped one.
+__device__ __forceinline__ f3 accumulate_filtered(const Params& P, f3 filtered, float pfx, float pfy,
+                                                  uint8_t acc_bits, uint8_t spp, f3 albedo,
+                                                  const float* __restrict__ acc_prev, int frame,
+                                                  f3* tone) {
+    f3 prev{0.f, 0.f, 0.f};
+    float alpha = 1.f;
+    if (frame > 0 && acc_bits > 0) {
+        const float flx = floorf(pfx), fly = floorf(pfy);
+        const int ix = (int)flx, iy = (int)fly;
+        const float fx = pfx - flx, fy = pfy - fly;
+        const float omx = 1.f - fx, omy = 1.f - fy;
+        const float wts[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
+        float total = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (acc_bits & (1 << i)) {
+                total = total + wts[i];
+                const f3 pc = ld3(acc_prev, (long)(iy + (i >> 1)) * P.width + ix + (i & 1));
+                prev.x = prev.x + wts[i] * pc.x;
+                prev.y = prev.y + wts[i] * pc.y;
+                prev.z = prev.z + wts[i] * pc.z;
+            }
+        }
+        if (total > 0.f) {
+            alpha = 1.f / (float)spp;
+            alpha = fmaxf(alpha, P.second_blend_alpha);
+            const float rt = 1.f / total;
+            prev.x = div_shared(prev.x, total, rt);
+            prev.y = div_shared(prev.y, total, rt);
+            prev.z = div_shared(prev.z, total, rt);
+        }
+    }
+    const float beta = 1.f - alpha;
+    const f3 a{alpha * filtered.x + beta * prev.x, alpha * filtered.y + beta * prev.y,
+               alpha * filtered.z + beta * prev.z};
+    const float g = 0.454545f;
+    tone->x = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.x * a.x), g), 0.f), 1.f);
+    tone->y = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.y * a.y), g), 0.f), 1.f);
+    tone->z = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.z * a.z), g), 0.f), 1.f);
+    return a;
+}
+
 
 }  // namespace bmfr

@@ -116,50 +116,6 @@ __global__ __launch_bounds__(256) void k_weighted_sum(Params P, const float* __r
 }
 
 // ---------------------------------------------------------------- stage 4 --
-// Temporal blend of the filtered colour, albedo remodulation and the
-// 1/2.2 gamma (bmfr.cl:761-857).  Returns the accumulated colour; *tone gets
-// the tone-mapped one.
-__device__ __forceinline__ f3 accumulate_filtered(const Params& P, f3 filtered, float pfx, float pfy,
-                                                  uint8_t acc_bits, uint8_t spp, f3 albedo,
-                                                  const float* __restrict__ acc_prev, int frame,
-                                                  f3* tone) {
-    f3 prev{0.f, 0.f, 0.f};
-    float alpha = 1.f;
-    if (frame > 0 && acc_bits > 0) {
-        const float flx = floorf(pfx), fly = floorf(pfy);
-        const int ix = (int)flx, iy = (int)fly;
-        const float fx = pfx - flx, fy = pfy - fly;
-        const float omx = 1.f - fx, omy = 1.f - fy;
-        const float wts[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
-        float total = 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (acc_bits & (1 << i)) {
-                total = total + wts[i];
-                const f3 pc = ld3(acc_prev, (long)(iy + (i >> 1)) * P.width + ix + (i & 1));
-                prev.x = prev.x + wts[i] * pc.x;
-                prev.y = prev.y + wts[i] * pc.y;
-                prev.z = prev.z + wts[i] * pc.z;
-            }
-        }
-        if (total > 0.f) {
-            alpha = 1.f / (float)spp;
-            alpha = fmaxf(alpha, P.second_blend_alpha);
-            prev.x = prev.x / total;
-            prev.y = prev.y / total;
-            prev.z = prev.z / total;
-        }
-    }
-    const float beta = 1.f - alpha;
-    const f3 a{alpha * filtered.x + beta * prev.x, alpha * filtered.y + beta * prev.y,
-               alpha * filtered.z + beta * prev.z};
-    const float g = 0.454545f;
-    tone->x = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.x * a.x), g), 0.f), 1.f);
-    tone->y = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.y * a.y), g), 0.f), 1.f);
-    tone->z = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.z * a.z), g), 0.f), 1.f);
-    return a;
-}
-
 __global__ __launch_bounds__(256) void k_accumulate_filtered(
     Params P, const float* __restrict__ filtered, const float2* __restrict__ prev_pixel,
     const uint8_t* __restrict__ accept, const float* __restrict__ albedo,
@@ -230,7 +186,8 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
             total = total + tw[i];
         }
     }
-    prev = f3{prev.x / total, prev.y / total, prev.z / total};
+    const float rt = 1.f / total;  // total can be 0 only in a degenerate case (bmfr.cl:962)
+    prev = f3{div_shared(prev.x, total, rt), div_shared(prev.y, total, rt), div_shared(prev.z, total, rt)};
     const f3 py = rgb_to_ycocg(prev);
     const f3 lo{(mnb.x + mnc.x) / 2.f, (mnb.y + mnc.y) / 2.f, (mnb.z + mnc.z) / 2.f};
     const f3 hi{(mxb.x + mxc.x) / 2.f, (mxb.y + mxc.y) / 2.f, (mxb.z + mxc.z) / 2.f};
@@ -301,6 +258,18 @@ __global__ __launch_bounds__(256) void k_fused_block(Params P, NoisyInputs in, C
             st3(tone_out, lin[s], tone);
         }
     }
+}
+
+// ------------------------------------------------------------ noise table --
+// add_random()'s noise term (bmfr.cl:173-182) depends only on the row, the
+// feature and the frame, never on the block; K1 reads it from this table
+// instead of re-hashing per element: table[(fb-1)*1024 + row] = random() - 0.5f
+// for fb = 1..B-4; the kernel forms NOISE_AMOUNT*2.f*that in double as upstream.
+__global__ __launch_bounds__(256) void k_noise_table(int frame, int buffers, float* __restrict__ table) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (buffers - 4) * kBlockPixels) return;
+    const int fb = 1 + i / kBlockPixels, r = i % kBlockPixels;
+    table[i] = hash_random((uint32_t)(r + fb * kBlockPixels + frame * buffers * kBlockPixels)) - 0.5f;
 }
 
 // ---------------------------------------------------------------- launch --
@@ -381,7 +350,13 @@ static hipError_t launch_fused_t(const Params& P, hipStream_t st, const FusedArg
 
 hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& A, hipEvent_t mid) {
     hipError_t e;
-    if (P.not_scaled == 4 && P.scaled == 6) e = launch_fused_t<4, 6>(P, st, A);
+    if (fused_wave_supported(P)) {
+        const int n = (P.buffers - 4) * kBlockPixels;
+        hipLaunchKernelGGL(k_noise_table, dim3((n + 255) / 256), dim3(256), 0, st, A.frame, P.buffers,
+                           A.noise_table);
+        e = launch_fused_wave(P, st, A);
+    }
+    else if (P.not_scaled == 4 && P.scaled == 6) e = launch_fused_t<4, 6>(P, st, A);
     else if (P.not_scaled == 4 && P.scaled == 9) e = launch_fused_t<4, 9>(P, st, A);
     else return hipErrorInvalidValue;
     if (e != hipSuccess) return e;

@@ -21,9 +21,12 @@ struct FusedArgs {
     float* acc_out;
     float* tone_out;
     float* result_out;
+    float* noise_table;  // (B-4) * 1024 floats, context-owned
 };
 
 bool fitter_supported(int not_scaled, int scaled);
+bool fused_wave_supported(const Params& P);
+hipError_t launch_fused_wave(const Params& P, hipStream_t st, const FusedArgs& A);
 
 hipError_t launch_accumulate_noisy(const Params& P, hipStream_t st, float2* prev_pixel, uint8_t* accept,
                                    const NoisyInputs& in, float* noisy_out, uint8_t* spp_cur, void* tmp,

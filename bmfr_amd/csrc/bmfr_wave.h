@@ -1,0 +1,117 @@
+// bmfr_wave.h -- one-wave-per-block building blocks (gfx950).
+//
+// A 32x32 block is owned by ONE wave64: lane l holds rows r = l + 64*j,
+// j = 0..15.  Upstream's fitter work-item t (256 per block, bmfr.cl:487-507)
+// owns rows t + 256*s, i.e. t = l + 64*m with j = m + 4*s, so every
+// per-work-item partial AND the first tree step (256 -> 64, bmfr.cl:32-33)
+// are in-register here.  The remaining steps (64 -> 8 -> 1) run on DPP row
+// shifts, gfx950's permlane16/32 swaps and readlanes, in upstream's exact
+// association -- no LDS, no barriers.
+#pragma once
+
+#include "bmfr_kernels.h"
+
+namespace bmfr {
+
+// lane l <- lane l+8 within its 16-lane row (valid for l % 16 < 8)
+__device__ __forceinline__ float dpp_shl8(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x108, 0xf, 0xf, true));
+}
+// lanes 0..15 <- lanes 16..31 (permlane16_swap: odd rows of arg0 <-> even rows of arg1)
+__device__ __forceinline__ float swap16_down(float v) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+    return __int_as_float(p[1]);
+}
+// lanes 0..31 <- lanes 32..63
+__device__ __forceinline__ float swap32_down(float v) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+    return __int_as_float(p[1]);
+}
+
+// Steps 64 -> 8 -> 1 of parallel_reduction_{sum,max,min} (bmfr.cl:35-42,
+// 55-63, 77-85) on the 64 step-2 values s (one per lane).  Wave-uniform result.
+template <RedOp OP>
+__device__ __forceinline__ float wave_tree(float s) {
+    const float a = dpp_shl8(s);       // s[l+8]
+    const float b = swap16_down(s);    // s[l+16]
+    const float c = dpp_shl8(b);       // s[l+24]
+    const float d = swap32_down(s);    // s[l+32]
+    const float e = dpp_shl8(d);       // s[l+40]
+    const float f = swap16_down(d);    // s[l+48]
+    const float h = dpp_shl8(f);       // s[l+56]
+    float x;
+    if constexpr (OP == RedOp::Sum) {
+        x = s + ((((((a + b) + c) + d) + e) + f) + h);
+    } else {
+        x = red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(s, a), b), c), d), e), f), h);
+    }
+    float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+#pragma unroll
+    for (int k = 1; k < 8; ++k) r = red<OP>(r, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), k)));
+    return r;
+}
+
+// Step 2 (256 -> 64, bmfr.cl:32-33 / 51-53 / 73-75) on the four partials of
+// upstream work-items l, l+64, l+128, l+192.
+template <RedOp OP>
+__device__ __forceinline__ float step2(const float (&p)[4]) {
+    if constexpr (OP == RedOp::Sum) return p[0] + ((p[1] + p[2]) + p[3]);
+    else return red<OP>(red<OP>(red<OP>(p[0], p[1]), p[2]), p[3]);
+}
+
+// K independent sums at once, for one wave: lane l holds the step-2 values
+// v[k] (= s[l] of reduction k).  Steps 64 -> 8 -> 1 (bmfr.cl:35-42) run as an
+// LDS transpose: lane (k, i) forms e_k[i] = s[i] + (((s[i+8] + s[i+16]) + ...)
+// + s[i+56]), lane k forms ((e_k[0] + e_k[1]) + ...) + e_k[7].  About 2K+40
+// instructions for all K sums, against ~30 per sum for wave_tree.
+// scratch: >= K*72 + K*8 + K floats of LDS.
+constexpr int kRowStride = 72;  // 64 + 8: lanes (k, i) of one 32-lane group hit distinct banks
+template <int K>
+__device__ __forceinline__ void lds_batch_sum(float (&v)[K], float* __restrict__ scratch, int l) {
+    float* S = scratch;
+    float* E = scratch + K * kRowStride;
+    float* R = E + K * 8;
+#pragma unroll
+    for (int k = 0; k < K; ++k) S[k * kRowStride + l] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int base = 0; base < K * 8; base += 64) {
+        const int idx = base + l;
+        if (idx < K * 8) {
+            const float* row = S + (idx >> 3) * kRowStride + (idx & 7);
+            float acc = row[8];
+#pragma unroll
+            for (int j = 2; j < 8; ++j) acc = acc + row[8 * j];
+            E[idx] = row[0] + acc;
+        }
+    }
+    __syncthreads();
+    if (l < K) {
+        float r = E[l * 8];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) r = r + E[l * 8 + i];
+        R[l] = r;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = R[k];
+}
+
+// Packed-half design matrix: A[f][j] for j = 0..15 in 8 registers per column.
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+template <int B>
+struct HalfMatrix {
+    h2 v[B][8];
+    __device__ __forceinline__ float get(int f, int j) const { return (float)v[f][j >> 1][j & 1]; }
+    __device__ __forceinline__ void set(int f, int j, float x) { v[f][j >> 1][j & 1] = (_Float16)x; }
+    // Zero-instruction fence: the compiler must assume column f changed, so it
+    // re-unpacks it on the next get() instead of keeping f32 copies alive
+    // across a reduction (the difference between fitting in VGPRs and spilling).
+    __device__ __forceinline__ void fence(int f) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(v[f][i]));
+    }
+};
+
+}  // namespace bmfr
