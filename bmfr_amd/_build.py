@@ -13,8 +13,9 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libbmfr.so")
+DIAG_LIB = os.path.join(HERE, "libbmfr_diag.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["bmfr_kernels.hip", "bmfr_fused_wave.hip", "bmfr_capi.hip", "bmfr_synth.hip"]
+SOURCES = ["bmfr_kernels.hip", "bmfr_fused.hip", "bmfr_capi.hip", "bmfr_synth.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-Wall", "-Wno-unused-function"]
 
@@ -25,15 +26,18 @@ def _deps_mtime() -> float:
     return max(os.path.getmtime(f) for f in files)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():
-        return LIB
-    objdir = os.path.join(HERE, "_obj")
+def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
+    """Build libbmfr.so (or, diag=True, libbmfr_diag.so: same library with
+    in-kernel phase timestamps compiled in, for profiling only)."""
+    lib = DIAG_LIB if diag else LIB
+    if not force and os.path.exists(lib) and os.path.getmtime(lib) >= _deps_mtime():
+        return lib
+    objdir = os.path.join(HERE, "_obj_diag" if diag else "_obj")
     os.makedirs(objdir, exist_ok=True)
 
     def compile_one(src: str) -> str:
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
-        cmd = [HIPCC, *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [HIPCC, *FLAGS, *(["-DBMFR_STAMPS"] if diag else []), "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
@@ -41,11 +45,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs], check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    import sys
+    print(build(force=True, verbose=True, diag="--diag" in sys.argv))

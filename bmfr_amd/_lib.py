@@ -13,7 +13,8 @@ import os
 import torch  # noqa: F401  (see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbmfr.so")
+# BMFR_LIB=diag selects the diagnostic build (in-kernel timestamps) for profiling.
+LIB_PATH = os.path.join(HERE, "libbmfr_diag.so" if os.environ.get("BMFR_LIB") == "diag" else "libbmfr.so")
 
 MAX_FEATURES = 16
 
@@ -96,6 +97,7 @@ SIGNATURES = {
     "bmfr_set_profiling": (_I, [_P, _I, _I]),
     "bmfr_get_profile": (_I, [_P, C.POINTER(FrameProfile), _I, C.POINTER(_I)]),
     "bmfr_synth_camera": (None, [_I, _I, _I, _F16, _F2]),
+    "bmfr_debug_stamps": (_I, [_P, _P, C.c_size_t]),  # include/bmfr_debug.h
     "bmfr_synth_frame_host": (_I, [_I, _I, _I, C.c_uint32, _P, _P, _P, _P, _P]),
     "bmfr_synth_frame_device": (_I, [_I, _I, _I, C.c_uint32, _P, _P, _P, _P, _P, _P]),
 }

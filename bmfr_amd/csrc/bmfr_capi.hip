@@ -10,6 +10,7 @@
 #include <cstring>
 
 #include "../../include/bmfr.h"
+#include "../../include/bmfr_debug.h"
 #include "bmfr_launch.h"
 
 using bmfr::Params;
@@ -27,6 +28,7 @@ struct bmfr_ctx {
     float* tone = nullptr;
     float2* prev_pixel = nullptr;
     float* noise_table = nullptr;
+    unsigned long long* stamps = nullptr;  // diagnostic: BMFR_STAMPS=1 with libbmfr_diag.so
     int cur = 0;
     bool has_frame = false;
     // Profiling ring: 3 events per frame (before K1, after K1, after K2).
@@ -203,6 +205,8 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
     }
     if (e == hipSuccess) e = hipMalloc(&c->tone, px * 3 * sizeof(float));
     if (e == hipSuccess) e = hipMalloc(&c->prev_pixel, px * sizeof(float2));
+    if (e == hipSuccess && std::getenv("BMFR_STAMPS"))
+        e = hipMalloc(&c->stamps, (size_t)sz.blocks * 8 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&c->noise_table, (size_t)bmfr::kMaxFeatures * bmfr::kBlockPixels * sizeof(float));
     if (e != hipSuccess) {
         bmfr_destroy(c);
@@ -227,6 +231,7 @@ bmfr_status bmfr_destroy(bmfr_ctx* c) {
     (void)hipFree(c->tone);
     (void)hipFree(c->prev_pixel);
     (void)hipFree(c->noise_table);
+    (void)hipFree(c->stamps);
     delete c;
     return BMFR_OK;
 }
@@ -337,6 +342,7 @@ bmfr_status bmfr_process_frame(bmfr_ctx* c, void* stream, const bmfr_frame_input
     A.tone_out = c->tone;
     A.result_out = c->result[cur];
     A.noise_table = c->noise_table;
+    A.stamps = c->stamps;
     const bmfr_status st = hip_status(bmfr::launch_fused_frame(c->P, as_stream(stream), A, ev ? ev[1] : nullptr));
     if (st != BMFR_OK) return st;
     if (ev) {
@@ -392,6 +398,14 @@ bmfr_status bmfr_get_profile(bmfr_ctx* c, bmfr_frame_profile* out, int max_frame
     }
     *count = n;
     return BMFR_OK;
+}
+
+bmfr_status bmfr_debug_stamps(const bmfr_ctx* c, unsigned long long* host, size_t count) {
+    if (!c || !host) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (!c->stamps) return BMFR_ERROR_UNSUPPORTED;
+    const size_t n = (size_t)c->sizes.blocks * 8;
+    return hip_status(hipMemcpy(host, c->stamps, (count < n ? count : n) * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost));
 }
 
 const float* bmfr_output(const bmfr_ctx* c) {

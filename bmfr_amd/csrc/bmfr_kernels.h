@@ -388,13 +388,12 @@ __device__ __forceinline__ void fit_block(float (&a)[NS + FS + 3][kSubs], FitLds
 }
 
 // --------------------------------------------------------------------------
-// Temporal blend of the filtered colour, albedo remodulation and the
-// 1/2.2 gamma (bmfr.cl:761-857).  Returns the accumulated colour; *tone gets
-// the tone-mapped one.
-__device__ __forceinline__ f3 accumulate_filtered(const Params& P, f3 filtered, float pfx, float pfy,
-                                                  uint8_t acc_bits, uint8_t spp, f3 albedo,
-                                                  const float* __restrict__ acc_prev, int frame,
-                                                  f3* tone) {
+// Temporal blend of the filtered colour (bmfr.cl:778-849): the accumulated
+// colour of a pixel, given its filtered colour, reprojection, accept bits and
+// spp and the previous accumulated frame.
+__device__ __forceinline__ f3 blend_filtered(const Params& P, f3 filtered, float pfx, float pfy,
+                                             uint8_t acc_bits, uint8_t spp,
+                                             const float* __restrict__ acc_prev, int frame) {
     f3 prev{0.f, 0.f, 0.f};
     float alpha = 1.f;
     if (frame > 0 && acc_bits > 0) {
@@ -424,14 +423,72 @@ __device__ __forceinline__ f3 accumulate_filtered(const Params& P, f3 filtered, 
         }
     }
     const float beta = 1.f - alpha;
-    const f3 a{alpha * filtered.x + beta * prev.x, alpha * filtered.y + beta * prev.y,
-               alpha * filtered.z + beta * prev.z};
-    const float g = 0.454545f;
-    tone->x = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.x * a.x), g), 0.f), 1.f);
-    tone->y = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.y * a.y), g), 0.f), 1.f);
-    tone->z = fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.z * a.z), g), 0.f), 1.f);
-    return a;
+    return f3{alpha * filtered.x + beta * prev.x, alpha * filtered.y + beta * prev.y,
+              alpha * filtered.z + beta * prev.z};
 }
 
+// Albedo remodulation + 1/2.2 gamma + clamp (bmfr.cl:851-856), with the
+// device library's powr exactly as the reference kernel calls it.
+__device__ __forceinline__ f3 tone_map(f3 albedo, f3 a) {
+    const float g = 0.454545f;
+    return f3{fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.x * a.x), g), 0.f), 1.f),
+              fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.y * a.y), g), 0.f), 1.f),
+              fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.z * a.z), g), 0.f), 1.f)};
+}
+
+// TAA for one pixel (bmfr.cl:873-973); `tone(dx, dy)` returns the tone-mapped
+// colour of an in-image neighbour.
+template <class Tone>
+__device__ __forceinline__ f3 taa_pixel(const Params& P, int x, int y, f3 me, float2 pf,
+                                        const float* __restrict__ prev_frame, int frame, Tone tone) {
+    const int W = P.width, H = P.height;
+    const float flx = floorf(pf.x), fly = floorf(pf.y);
+    const int ix = (int)flx, iy = (int)fly;
+    if (frame == 0 || ix < -1 || iy < -1 || ix >= W || iy >= H) return me;  // bmfr.cl:884-890
+    f3 mnb{INFINITY, INFINITY, INFINITY}, mnc = mnb;
+    f3 mxb{-INFINITY, -INFINITY, -INFINITY}, mxc = mxb;
+#pragma unroll
+    for (int dy = -1; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = -1; dx < 2; ++dx) {  // bmfr.cl:897-920
+            const int sx = x + dx, sy = y + dy;
+            if (sx >= 0 && sy >= 0 && sx < W && sy < H) {
+                f3 s = (dx == 0 && dy == 0) ? me : tone(dx, dy);
+                s = rgb_to_ycocg(s);
+                if (dx == 0 || dy == 0) {
+                    mnc = f3{fminf(mnc.x, s.x), fminf(mnc.y, s.y), fminf(mnc.z, s.z)};
+                    mxc = f3{fmaxf(mxc.x, s.x), fmaxf(mxc.y, s.y), fmaxf(mxc.z, s.z)};
+                }
+                mnb = f3{fminf(mnb.x, s.x), fminf(mnb.y, s.y), fminf(mnb.z, s.z)};
+                mxb = f3{fmaxf(mxb.x, s.x), fmaxf(mxb.y, s.y), fmaxf(mxb.z, s.z)};
+            }
+        }
+    f3 prev{0.f, 0.f, 0.f};
+    float total = 0.f;
+    const float fx = pf.x - flx, fy = pf.y - fly;
+    const float omx = 1.f - fx, omy = 1.f - fy;
+    const float tw[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // bmfr.cl:929-960
+        const bool okx = (i & 1) ? (ix < W - 1) : (ix >= 0);
+        const bool oky = (i >> 1) ? (iy < H - 1) : (iy >= 0);
+        if (okx && oky) {
+            const f3 pc = ld3(prev_frame, (long)(iy + (i >> 1)) * W + ix + (i & 1));
+            prev.x = prev.x + tw[i] * pc.x;
+            prev.y = prev.y + tw[i] * pc.y;
+            prev.z = prev.z + tw[i] * pc.z;
+            total = total + tw[i];
+        }
+    }
+    const float rt = 1.f / total;  // total can be 0 only in a degenerate case (bmfr.cl:962)
+    prev = f3{div_shared(prev.x, total, rt), div_shared(prev.y, total, rt), div_shared(prev.z, total, rt)};
+    const f3 py = rgb_to_ycocg(prev);
+    const f3 lo{(mnb.x + mnc.x) / 2.f, (mnb.y + mnc.y) / 2.f, (mnb.z + mnc.z) / 2.f};
+    const f3 hi{(mxb.x + mxc.x) / 2.f, (mxb.y + mxc.y) / 2.f, (mxb.z + mxc.z) / 2.f};
+    const f3 cl{fminf(fmaxf(py.x, lo.x), hi.x), fminf(fmaxf(py.y, lo.y), hi.y), fminf(fmaxf(py.z, lo.z), hi.z)};
+    const f3 pr = ycocg_to_rgb(cl);
+    const float a = P.taa_blend_alpha, b = 1.f - a;
+    return f3{a * me.x + b * pr.x, a * me.y + b * pr.y, a * me.z + b * pr.z};
+}
 
 }  // namespace bmfr

@@ -126,11 +126,10 @@ __global__ __launch_bounds__(256) void k_accumulate_filtered(
     if (x >= P.width || y >= P.height) return;
     const long lin = (long)y * P.width + x;
     const float2 pp = prev_pixel[lin];
-    f3 tone;
-    const f3 a = accumulate_filtered(P, ld3(filtered, lin), pp.x, pp.y, frame > 0 ? accept[lin] : 0,
-                                     spp[lin], ld3(albedo, lin), acc_prev, frame, &tone);
+    const f3 a = blend_filtered(P, ld3(filtered, lin), pp.x, pp.y, frame > 0 ? accept[lin] : 0, spp[lin],
+                                acc_prev, frame);
     st3(acc, lin, a);
-    st3(tone_mapped, lin, tone);
+    st3(tone_mapped, lin, tone_map(ld3(albedo, lin), a));
 }
 
 // ---------------------------------------------------------------- stage 5 --
@@ -141,64 +140,59 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
     if (x >= P.width || y >= P.height) return;
-    const int W = P.width, H = P.height;
-    const long lin = (long)y * W + x;
-    const f3 me = ld3(new_frame, lin);
-    const float2 pf = prev_pixel[lin];
-    const float flx = floorf(pf.x), fly = floorf(pf.y);
-    const int ix = (int)flx, iy = (int)fly;
-    if (frame == 0 || ix < -1 || iy < -1 || ix >= W || iy >= H) {  // bmfr.cl:884-890
-        st3(result, lin, me);
-        return;
-    }
-    f3 mnb{INFINITY, INFINITY, INFINITY}, mnc = mnb;
-    f3 mxb{-INFINITY, -INFINITY, -INFINITY}, mxc = mxb;
-#pragma unroll
-    for (int dy = -1; dy < 2; ++dy)
-#pragma unroll
-        for (int dx = -1; dx < 2; ++dx) {  // bmfr.cl:897-920
-            const int sx = x + dx, sy = y + dy;
-            if (sx >= 0 && sy >= 0 && sx < W && sy < H) {
-                f3 s = (dx == 0 && dy == 0) ? me : ld3(new_frame, (long)sy * W + sx);
-                s = rgb_to_ycocg(s);
-                if (dx == 0 || dy == 0) {
-                    mnc = f3{fminf(mnc.x, s.x), fminf(mnc.y, s.y), fminf(mnc.z, s.z)};
-                    mxc = f3{fmaxf(mxc.x, s.x), fmaxf(mxc.y, s.y), fmaxf(mxc.z, s.z)};
-                }
-                mnb = f3{fminf(mnb.x, s.x), fminf(mnb.y, s.y), fminf(mnb.z, s.z)};
-                mxb = f3{fmaxf(mxb.x, s.x), fmaxf(mxb.y, s.y), fmaxf(mxb.z, s.z)};
-            }
-        }
-    f3 prev{0.f, 0.f, 0.f};
-    float total = 0.f;
-    const float fx = pf.x - flx, fy = pf.y - fly;
-    const float omx = 1.f - fx, omy = 1.f - fy;
-    const float tw[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {  // bmfr.cl:929-960
-        const bool okx = (i & 1) ? (ix < W - 1) : (ix >= 0);
-        const bool oky = (i >> 1) ? (iy < H - 1) : (iy >= 0);
-        if (okx && oky) {
-            const f3 pc = ld3(prev_frame, (long)(iy + (i >> 1)) * W + ix + (i & 1));
-            prev.x = prev.x + tw[i] * pc.x;
-            prev.y = prev.y + tw[i] * pc.y;
-            prev.z = prev.z + tw[i] * pc.z;
-            total = total + tw[i];
-        }
-    }
-    const float rt = 1.f / total;  // total can be 0 only in a degenerate case (bmfr.cl:962)
-    prev = f3{div_shared(prev.x, total, rt), div_shared(prev.y, total, rt), div_shared(prev.z, total, rt)};
-    const f3 py = rgb_to_ycocg(prev);
-    const f3 lo{(mnb.x + mnc.x) / 2.f, (mnb.y + mnc.y) / 2.f, (mnb.z + mnc.z) / 2.f};
-    const f3 hi{(mxb.x + mxc.x) / 2.f, (mxb.y + mxc.y) / 2.f, (mxb.z + mxc.z) / 2.f};
-    const f3 cl{fminf(fmaxf(py.x, lo.x), hi.x), fminf(fmaxf(py.y, lo.y), hi.y),
-                fminf(fmaxf(py.z, lo.z), hi.z)};
-    const f3 pr = ycocg_to_rgb(cl);
-    const float a = P.taa_blend_alpha, b = 1.f - a;
-    st3(result, lin, f3{a * me.x + b * pr.x, a * me.y + b * pr.y, a * me.z + b * pr.z});
+    const long lin = (long)y * P.width + x;
+    const f3 r = taa_pixel(P, x, y, ld3(new_frame, lin), prev_pixel[lin], prev_frame, frame,
+                           [&](int dx, int dy) { return ld3(new_frame, lin + (long)dy * P.width + dx); });
+    st3(result, lin, r);
 }
 
-// ------------------------------------------------------------ fused K1 ----
+// ----------------------------------------------------- fused K2: tone + TAA --
+// One 64x16 tile per 256-thread work-group.  The tile and a 1-pixel halo are
+// tone-mapped from the accumulated filtered colour and the albedo straight
+// into LDS (the fused K1 never writes a tone-mapped frame), then TAA reads its
+// 3x3 neighbourhoods from LDS.
+constexpr int kTaaW = 64, kTaaH = 16;
+__global__ __launch_bounds__(256) void k_tone_taa(Params P, const float* __restrict__ acc,
+                                                  const float* __restrict__ albedo,
+                                                  const float2* __restrict__ prev_pixel,
+                                                  float* __restrict__ result,
+                                                  const float* __restrict__ prev_frame, int frame) {
+    constexpr int HW = kTaaW + 2, HH = kTaaH + 2, N = HW * HH;
+    __shared__ float T[3][N];
+    const int t = threadIdx.x;
+    const int x0 = blockIdx.x * kTaaW, y0 = blockIdx.y * kTaaH;
+    for (int i = t; i < N; i += 256) {
+        const int x = x0 - 1 + i % HW, y = y0 - 1 + i / HW;
+        if (x >= 0 && y >= 0 && x < P.width && y < P.height) {
+            const long lin = (long)y * P.width + x;
+            const f3 c = tone_map(ld3(albedo, lin), ld3(acc, lin));
+            T[0][i] = c.x;
+            T[1][i] = c.y;
+            T[2][i] = c.z;
+        }
+    }
+    __syncthreads();
+    const int tx = t & (kTaaW - 1);
+#pragma unroll
+    for (int k = 0; k < kTaaH / 4; ++k) {
+        const int ty = (t >> 6) + 4 * k;
+        const int x = x0 + tx, y = y0 + ty;
+        if (x < P.width && y < P.height) {
+            const int c = (ty + 1) * HW + tx + 1;
+            const long lin = (long)y * P.width + x;
+            const f3 me{T[0][c], T[1][c], T[2][c]};
+            const f3 r = taa_pixel(P, x, y, me, prev_pixel[lin], prev_frame, frame, [&](int dx, int dy) {
+                const int n = c + dy * HW + dx;
+                return f3{T[0][n], T[1][n], T[2][n]};
+            });
+            st3(result, lin, r);
+        }
+    }
+}
+
+// ------------------------------------------- generic-feature fused K1 ----
+// Fallback K1 for feature lists other than the canonical ones (runtime
+// feature codes); the canonical lists use k_fused (bmfr_fused.hip).
 template <int NS, int FS, bool HALF>
 __global__ __launch_bounds__(256) void k_fused_block(Params P, NoisyInputs in, Camera cam, int frame,
                                                      const float* __restrict__ albedo,
@@ -250,12 +244,10 @@ __global__ __launch_bounds__(256) void k_fused_block(Params P, NoisyInputs in, C
         const uint32_t fl = flags >> (8 * s);
         if (fl & 1u) {
             const f3 filtered = weighted_color(P, L.weights, L.minmax, n_keep[s], p_keep[s]);
-            f3 tone;
-            const f3 acc = accumulate_filtered(P, filtered, pfx[s], pfy[s], (uint8_t)((fl >> 1) & 15u),
-                                               (uint8_t)(spps >> (8 * s)), ld3(albedo, lin[s]),
-                                               acc_prev, frame, &tone);
+            const f3 acc = blend_filtered(P, filtered, pfx[s], pfy[s], (uint8_t)((fl >> 1) & 15u),
+                                          (uint8_t)(spps >> (8 * s)), acc_prev, frame);
             st3(acc_out, lin[s], acc);
-            st3(tone_out, lin[s], tone);
+            st3(tone_out, lin[s], tone_map(ld3(albedo, lin[s]), acc));
         }
     }
 }
@@ -350,13 +342,19 @@ static hipError_t launch_fused_t(const Params& P, hipStream_t st, const FusedArg
 
 hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& A, hipEvent_t mid) {
     hipError_t e;
-    if (fused_wave_supported(P)) {
+    if (fused_supported(P)) {
         const int n = (P.buffers - 4) * kBlockPixels;
         hipLaunchKernelGGL(k_noise_table, dim3((n + 255) / 256), dim3(256), 0, st, A.frame, P.buffers,
                            A.noise_table);
-        e = launch_fused_wave(P, st, A);
+        e = launch_fused_k1(P, st, A);
+        if (e != hipSuccess) return e;
+        if (mid) (void)hipEventRecord(mid, st);
+        const dim3 grd((P.width + kTaaW - 1) / kTaaW, (P.height + kTaaH - 1) / kTaaH);
+        hipLaunchKernelGGL(k_tone_taa, grd, dim3(256), 0, st, P, A.acc_out, A.albedo, A.prev_pixel_out,
+                           A.result_out, A.result_prev, A.frame);
+        return hipGetLastError();
     }
-    else if (P.not_scaled == 4 && P.scaled == 6) e = launch_fused_t<4, 6>(P, st, A);
+    if (P.not_scaled == 4 && P.scaled == 6) e = launch_fused_t<4, 6>(P, st, A);
     else if (P.not_scaled == 4 && P.scaled == 9) e = launch_fused_t<4, 9>(P, st, A);
     else return hipErrorInvalidValue;
     if (e != hipSuccess) return e;

@@ -22,11 +22,12 @@ struct FusedArgs {
     float* tone_out;
     float* result_out;
     float* noise_table;  // (B-4) * 1024 floats, context-owned
+    unsigned long long* stamps;  // diagnostic build: 8 timestamps per block, or null
 };
 
 bool fitter_supported(int not_scaled, int scaled);
-bool fused_wave_supported(const Params& P);
-hipError_t launch_fused_wave(const Params& P, hipStream_t st, const FusedArgs& A);
+bool fused_supported(const Params& P);
+hipError_t launch_fused_k1(const Params& P, hipStream_t st, const FusedArgs& A);
 
 hipError_t launch_accumulate_noisy(const Params& P, hipStream_t st, float2* prev_pixel, uint8_t* accept,
                                    const NoisyInputs& in, float* noisy_out, uint8_t* spp_cur, void* tmp,

@@ -174,8 +174,10 @@ const float *bmfr_output(const bmfr_ctx *ctx);
 
 /* Device pointers to the context's temporal state of the last frame, for
  * inspection / multi-GPU halo exchange: accumulated noisy colour (float3),
- * spp (u8), accumulated filtered colour (float3), tone-mapped frame (float3),
- * prev-frame pixel (float2), accept bits (u8). */
+ * spp (u8), accumulated filtered colour (float3), prev-frame pixel (float2).
+ * tone_mapped is only materialised by the generic-feature fallback (the
+ * canonical path tone-maps inside the TAA kernel) and accept bits never are
+ * (NULL). */
 typedef struct bmfr_state_view {
     float *noisy_accumulated;
     uint8_t *spp;

@@ -11,7 +11,7 @@ silently compared.  Per frame the fixture keeps
   * tone / result (powr-dependent) as float64 sums and an 8192-element
     strided sample (compared with a tolerance on the CPU side).
 
-Usage (GPU box): python tests/golden/make_golden.py [config ...]
+Usage (GPU box): python tests/golden/make_golden.py [--out DIR] [config ...]
 """
 from __future__ import annotations
 
@@ -32,7 +32,7 @@ from ref_configs import REF_CONFIGS  # noqa: E402
 from seq_util import EXACT_KEYS, POWR_KEYS, digest, frame_inputs, input_digest, run_loop, sample_idx  # noqa: E402
 
 
-def make(name: str) -> str:
+def make(name: str, out_dir: str = HERE) -> str:
     rc = REF_CONFIGS[name]
     frames = run_loop(ref_run.RefLoop(rc, "strict"), rc, rc.frames,
                       to_device=lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda(),
@@ -51,12 +51,17 @@ def make(name: str) -> str:
             st[k] = {"sum": float(a.sum()), "sumsq": float((a * a).sum())}
             arrays[f"{k}_sample_{f}"] = fr[k][sample_idx(fr[k].size)]
         meta["stats"].append(st)
-    path = os.path.join(HERE, f"{name}.npz")
+    os.makedirs(out_dir, exist_ok=True)
+    path = os.path.join(out_dir, f"{name}.npz")
     np.savez_compressed(path, meta=np.frombuffer(json.dumps(meta).encode(), np.uint8), **arrays)
     return path
 
 
 if __name__ == "__main__":
-    names = sys.argv[1:] or list(REF_CONFIGS)
-    for n in names:
-        print(make(n), flush=True)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*")
+    ap.add_argument("--out", default=HERE, help="output directory (default: tests/golden)")
+    a = ap.parse_args()
+    for n in a.configs or list(REF_CONFIGS):
+        print(make(n, a.out), flush=True)

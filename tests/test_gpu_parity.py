@@ -101,7 +101,6 @@ def test_fused_frame_matches_stages_bitwise(name, gpu):
             "noisy": den.copy_state("noisy_accumulated", torch.empty(3 * n, device="cuda")),
             "spp": den.copy_state("spp", torch.empty(n, dtype=torch.uint8, device="cuda")),
             "acc": den.copy_state("filtered_accumulated", torch.empty(3 * n, device="cuda")),
-            "tone": den.copy_state("tone_mapped", torch.empty(3 * n, device="cuda")),
             "prev_pixel": den.copy_state("prev_frame_pixel", torch.empty(2 * n, device="cuda")),
         }
         torch.cuda.synchronize()

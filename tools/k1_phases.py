@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Per-phase timing of the fused K1 kernel from in-kernel timestamps.
+
+Needs the diagnostic library (python bmfr_amd/_build.py --diag) and runs with
+BMFR_LIB=diag BMFR_STAMPS=1 (set here before importing bmfr_amd).  Prints,
+over all blocks of the last frame, the median / mean shader cycles spent in
+each phase and the spread of block start times.
+"""
+import os
+import sys
+
+os.environ["BMFR_LIB"] = "diag"
+os.environ["BMFR_STAMPS"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import ctypes as C  # noqa: E402
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bmfr_amd  # noqa: E402
+
+W, H = (int(x) for x in (sys.argv[1:3] if len(sys.argv) > 2 else (3840, 2160)))
+cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H)
+den = bmfr_amd.Denoiser(cfg)
+frames = [bmfr_amd.synth_frame_device(W, H, f) for f in range(4)]
+for f in range(4):
+    vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+    _, jit = bmfr_amd.synth_camera(W, H, f)
+    fr = frames[f]
+    den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, f)
+torch.cuda.synchronize()
+G = den.sizes.blocks
+buf = np.zeros(G * 8, np.uint64)
+rc = den.lib.bmfr_debug_stamps(den.handle, buf.ctypes.data_as(C.c_void_p), buf.size)
+assert rc == 0, rc
+st = buf.reshape(G, 8).astype(np.int64)
+names = ["accumulate_noisy", "min/max scale", "QR", "back-subst", "weighted+blend"]
+d = np.diff(st[:, :6], axis=1)
+tot = st[:, 5] - st[:, 0]
+print(f"{W}x{H}: {G} blocks; block lifetime cycles median {np.median(tot):.0f} mean {tot.mean():.0f}")
+for i, n in enumerate(names):
+    print(f"  {n:18s} median {np.median(d[:, i]):8.0f}  mean {d[:, i].mean():8.0f}  share {d[:, i].sum() / tot.sum():.2%}")
+span = st[:, 5].max() - st[:, 0].min()
+print(f"  kernel span (cycles) {span}, start spread {st[:, 0].max() - st[:, 0].min()}")
