@@ -323,11 +323,13 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, NoisyInputs in, Ca
     Rows<B, HALF> A;
     uint32_t state = 0;  // per s: owner (bit 0), accept bits (1-4), spp (8-15) -> 16 bits each ...
     uint32_t state_hi = 0;
+    NoisyCur cur[kSubs];  // current-frame loads of all four rows go out first
+#pragma unroll
+    for (int s = 0; s < kSubs; ++s)
+        cur[s] = noisy_load_current(P, in, bx * kEdge + (t & (kEdge - 1)), by * kEdge + (t >> 5) + 8 * s, frame);
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {
-        const int gx = bx * kEdge + (t & (kEdge - 1));
-        const int gy = by * kEdge + (t >> 5) + 8 * s;
-        const NoisyItem it = noisy_item(P, in, cam, gx, gy, frame);
+        const NoisyItem it = noisy_item_spec(P, in, cam, cur[s], frame);
 #pragma unroll
         for (int f = 0; f < B; ++f) {
             float v;
@@ -404,18 +406,30 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, NoisyInputs in, Ca
     int t3 = t;  // opaque copy: recompute phase-1 addresses instead of keeping them live
     asm volatile("" : "+v"(t3));
     const int2 off = kBlockOffsets[frame & 15];
+    // All loads of the four rows first (normal, position, reprojection), then
+    // the colours and the previous accumulation's taps.
+    f3 n[kSubs], pos[kSubs];
+    float2 pp[kSubs];
+    long lin[kSubs];
+    uint32_t bits[kSubs];
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {
-        const uint32_t bits = (s < 2 ? state >> (16 * s) : state_hi >> (16 * (s - 2))) & 0xffffu;
-        if (bits & 1u) {
-            const int px = bx * kEdge + (t3 & (kEdge - 1)) - kEdge / 2 + off.x;
-            const int py = by * kEdge + (t3 >> 5) + 8 * s - kEdge / 2 + off.y;
-            const long lin = (long)py * P.width + px;
-            const f3 n = ld3(in.n_cur, lin), pos = ld3(in.p_cur, lin);
+        bits[s] = (s < 2 ? state >> (16 * s) : state_hi >> (16 * (s - 2))) & 0xffffu;
+        const int px = bx * kEdge + (t3 & (kEdge - 1)) - kEdge / 2 + off.x;
+        const int py = by * kEdge + (t3 >> 5) + 8 * s - kEdge / 2 + off.y;
+        // non-owned rows (margins) read a valid pixel and are then skipped
+        lin[s] = (bits[s] & 1u) ? (long)py * P.width + px : 0;
+        n[s] = ld3(in.n_cur, lin[s]);
+        pos[s] = ld3(in.p_cur, lin[s]);
+        pp[s] = prev_pixel_out[lin[s]];
+    }
+#pragma unroll
+    for (int s = 0; s < kSubs; ++s) {
+        if (bits[s] & 1u) {
             f3 c{0.f, 0.f, 0.f};
 #pragma unroll
             for (int f = 0; f < B - 3; ++f) {
-                float v = feature_value(f, n, pos);
+                float v = feature_value(f, n[s], pos[s]);
                 if (f >= NS) {
                     const float bmin = L.mm[3 * (f - NS)], bmax = L.mm[3 * (f - NS) + 1];
                     const float d = bmax - bmin;
@@ -429,9 +443,9 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, NoisyInputs in, Ca
             c.x = c.x < 0.f ? 0.f : c.x;
             c.y = c.y < 0.f ? 0.f : c.y;
             c.z = c.z < 0.f ? 0.f : c.z;
-            const float2 pp = prev_pixel_out[lin];
-            st3(acc_out, lin,
-                blend_filtered(P, c, pp.x, pp.y, (uint8_t)((bits >> 1) & 15u), (uint8_t)(bits >> 8), acc_prev, frame));
+            st3(acc_out, lin[s],
+                blend_filtered(P, c, pp[s].x, pp[s].y, (uint8_t)((bits[s] >> 1) & 15u), (uint8_t)(bits[s] >> 8),
+                               acc_prev, frame));
         }
     }
 #ifdef BMFR_STAMPS

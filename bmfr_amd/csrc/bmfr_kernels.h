@@ -185,6 +185,113 @@ __device__ __forceinline__ NoisyItem noisy_item(const Params& P, const NoisyInpu
     return o;
 }
 
+// The same work-item with every load issued up front: the previous-frame
+// position, normal, colour and spp of all four bilinear taps are fetched
+// unconditionally (out-of-image taps at a clamped in-image address, then
+// ignored), so a pixel costs two dependent memory round trips instead of up
+// to four.  The arithmetic, its order and the results are noisy_item's.
+struct NoisyCur {
+    f3 wp, nrm, cur;
+    int px, py;
+    bool owner;
+};
+__device__ __forceinline__ NoisyCur noisy_load_current(const Params& P, const NoisyInputs& in, int gx, int gy,
+                                                       int frame) {
+    NoisyCur c;
+    const int2 off = kBlockOffsets[frame & 15];
+    const int ux = gx - kEdge / 2 + off.x, uy = gy - kEdge / 2 + off.y;
+    c.px = mirror(ux, P.width);
+    c.py = mirror(uy, P.height);
+    c.owner = ux >= 0 && ux < P.width && uy >= 0 && uy < P.height;
+    const long lin = (long)c.py * P.width + c.px;
+    c.wp = ld3(in.p_cur, lin);
+    c.nrm = ld3(in.n_cur, lin);
+    c.cur = ld3(in.noisy_cur, lin);
+    return c;
+}
+
+__device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const NoisyInputs& in, const Camera& cam,
+                                                     const NoisyCur& c, int frame) {
+    NoisyItem o;
+    o.owner = c.owner;
+    o.lin = (long)c.py * P.width + c.px;
+    o.n = c.nrm;
+    o.p = c.wp;
+    const f3 wp = c.wp, nrm = c.nrm, cur = c.cur;
+    float pfx = (float)c.px, pfy = (float)c.py;
+    uint8_t accept = 0;
+    float alpha = 1.f;
+    f3 prev{0.f, 0.f, 0.f};
+    float sample_spp = 0.f;
+    if (frame > 0) {
+        const float* M = cam.m;
+        float u = dot4(M[0], M[4], M[8], M[12], wp.x, wp.y, wp.z, 1.f);
+        float v = dot4(M[1], M[5], M[9], M[13], wp.x, wp.y, wp.z, 1.f);
+        const float w = dot4(M[3], M[7], M[11], M[15], wp.x, wp.y, wp.z, 1.f);
+        const float rw = 1.f / w;
+        u = div_shared(u, w, rw);
+        v = div_shared(v, w, rw);
+        u = u + 1.f;
+        v = v + 1.f;
+        u = u / 2.f;
+        v = v / 2.f;
+        pfx = u * (float)P.width - cam.jx;
+        pfy = v * (float)P.height - (1 - cam.jy);
+        const float flx = floorf(pfx), fly = floorf(pfy);
+        // Clamp before converting: a far-off reprojection must not overflow int.
+        const int ix = (int)fminf(fmaxf(flx, -2.f), (float)P.width + 1.f);
+        const int iy = (int)fminf(fmaxf(fly, -2.f), (float)P.height + 1.f);
+        const float fx = pfx - flx, fy = pfy - fly;
+        const float omx = 1.f - fx, omy = 1.f - fy;
+        const float wts[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
+        f3 pp[4], pn[4], pc[4];
+        float sp[4];
+        bool inb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int sx = ix + (i & 1), sy = iy + (i >> 1);
+            inb[i] = sx >= 0 && sy >= 0 && sx < P.width && sy < P.height;
+            const long s = (long)min(max(sy, 0), P.height - 1) * P.width + min(max(sx, 0), P.width - 1);
+            pp[i] = ld3(in.p_prev, s);
+            pn[i] = ld3(in.n_prev, s);
+            pc[i] = ld3(in.noisy_prev, s);
+            sp[i] = (float)in.spp_prev[s];
+        }
+        float total = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // bmfr.cl:374-419
+            const f3 d{pp[i].x - wp.x, pp[i].y - wp.y, pp[i].z - wp.z};
+            const f3 dn{pn[i].x - nrm.x, pn[i].y - nrm.y, pn[i].z - nrm.z};
+            if (inb[i] && dot3(d, d) < P.position_limit_sq && dot3(dn, dn) < P.normal_limit_sq) {
+                accept |= (uint8_t)(1 << i);
+                sample_spp = sample_spp + wts[i] * sp[i];
+                prev.x = prev.x + wts[i] * pc[i].x;
+                prev.y = prev.y + wts[i] * pc[i].y;
+                prev.z = prev.z + wts[i] * pc[i].z;
+                total = total + wts[i];
+            }
+        }
+        if (total > 0.f) {  // bmfr.cl:421-429
+            const float rt = 1.f / total;
+            prev.x = div_shared(prev.x, total, rt);
+            prev.y = div_shared(prev.y, total, rt);
+            prev.z = div_shared(prev.z, total, rt);
+            sample_spp = div_shared(sample_spp, total, rt);
+            alpha = 1.f / (sample_spp + 1.f);
+            alpha = fmaxf(alpha, P.blend_alpha);
+        }
+    }
+    uint8_t new_spp = 1;  // bmfr.cl:433-442
+    if (alpha < 1.f) new_spp = sample_spp > 254.f ? 255 : (uint8_t)((int)rintf(sample_spp) + 1);
+    const float beta = 1.f - alpha;
+    o.color = f3{alpha * cur.x + beta * prev.x, alpha * cur.y + beta * prev.y, alpha * cur.z + beta * prev.z};
+    o.pfx = pfx;
+    o.pfy = pfy;
+    o.accept = accept;
+    o.spp = new_spp;
+    return o;
+}
+
 // tmp_data value of feature f for an item (bmfr.cl:448-473): NaN -> 0, and
 // the +-65504 clamp when the matrix is kept in half.
 __device__ __forceinline__ float design_value(const Params& P, int f, const NoisyItem& it) {

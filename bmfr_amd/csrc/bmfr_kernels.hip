@@ -161,11 +161,21 @@ __global__ __launch_bounds__(256) void k_tone_taa(Params P, const float* __restr
     __shared__ float T[3][N];
     const int t = threadIdx.x;
     const int x0 = blockIdx.x * kTaaW, y0 = blockIdx.y * kTaaH;
-    for (int i = t; i < N; i += 256) {
-        const int x = x0 - 1 + i % HW, y = y0 - 1 + i / HW;
-        if (x >= 0 && y >= 0 && x < P.width && y < P.height) {
-            const long lin = (long)y * P.width + x;
-            const f3 c = tone_map(ld3(albedo, lin), ld3(acc, lin));
+    constexpr int ITER = (N + 255) / 256;
+    f3 al[ITER], ac[ITER];  // all tile loads in flight before any tone mapping
+#pragma unroll
+    for (int k = 0; k < ITER; ++k) {
+        const int i = t + 256 * k;
+        const int x = min(max(x0 - 1 + i % HW, 0), P.width - 1), y = min(max(y0 - 1 + i / HW, 0), P.height - 1);
+        const long lin = (long)y * P.width + x;
+        al[k] = ld3(albedo, lin);
+        ac[k] = ld3(acc, lin);
+    }
+#pragma unroll
+    for (int k = 0; k < ITER; ++k) {
+        const int i = t + 256 * k;
+        if (i < N) {
+            const f3 c = tone_map(al[k], ac[k]);  // clamped halo pixels are never read
             T[0][i] = c.x;
             T[1][i] = c.y;
             T[2][i] = c.z;
@@ -173,6 +183,12 @@ __global__ __launch_bounds__(256) void k_tone_taa(Params P, const float* __restr
     }
     __syncthreads();
     const int tx = t & (kTaaW - 1);
+    float2 pf[kTaaH / 4];
+#pragma unroll
+    for (int k = 0; k < kTaaH / 4; ++k) {
+        const int x = min(x0 + tx, P.width - 1), y = min(y0 + (t >> 6) + 4 * k, P.height - 1);
+        pf[k] = prev_pixel[(long)y * P.width + x];
+    }
 #pragma unroll
     for (int k = 0; k < kTaaH / 4; ++k) {
         const int ty = (t >> 6) + 4 * k;
@@ -181,7 +197,7 @@ __global__ __launch_bounds__(256) void k_tone_taa(Params P, const float* __restr
             const int c = (ty + 1) * HW + tx + 1;
             const long lin = (long)y * P.width + x;
             const f3 me{T[0][c], T[1][c], T[2][c]};
-            const f3 r = taa_pixel(P, x, y, me, prev_pixel[lin], prev_frame, frame, [&](int dx, int dy) {
+            const f3 r = taa_pixel(P, x, y, me, pf[k], prev_frame, frame, [&](int dx, int dy) {
                 const int n = c + dy * HW + dx;
                 return f3{T[0][n], T[1][n], T[2][n]};
             });
