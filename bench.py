@@ -37,12 +37,13 @@ import torch.distributed as dist  # noqa: E402
 import bmfr_amd  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# Algorithmic bytes per pixel (SURVEY.md §8d, 18*s + 74 with s = 4 for f32 planes):
-#   K1 reads noisy/normal/position/albedo (48) + previous normal/position (24)
+# Algorithmic bytes per pixel (SURVEY.md §8d, 18*s + 74 with s = 4 for f32 planes),
+# split over the two kernels by which one touches each compulsory byte:
+#   K1 reads noisy/normal/position (36) + previous normal/position (24)
 #   + accumulated noisy (12) + spp (1) + accumulated filtered (12) and writes
-#   accumulated noisy (12) + spp (1) + accumulated filtered (12) = 122;
-#   K2 reads the previous TAA output (12) and writes the output (12) = 24.
-K1_BYTES_PER_PX = 122
+#   accumulated noisy (12) + spp (1) + accumulated filtered (12) = 110;
+#   K2 reads albedo (12) + the previous TAA output (12), writes the output (12) = 36.
+K1_BYTES_PER_PX = 110
 FRAME_BYTES_PER_PX = 146
 
 

@@ -296,8 +296,10 @@ __device__ __forceinline__ void back_substitute(K1Lds<B>& L, int t) {
     if (x < B - 3) L.weights[x * 3 + ch] = R[((RE - 1) * RE + x) * 3 + ch];
 }
 
-template <int NS, int FS, bool HALF>
+template <int NS, int FS, bool HALF, bool TONE>
 __global__ __launch_bounds__(kThreads) void k_fused(Params P, NoisyInputs in, Camera cam, int frame,
+                                                    const float* __restrict__ albedo,
+                                                    float* __restrict__ tone_out,
                                                     const float* __restrict__ acc_prev,
                                                     float* __restrict__ noisy_out,
                                                     uint8_t* __restrict__ spp_out,
@@ -408,7 +410,7 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, NoisyInputs in, Ca
     const int2 off = kBlockOffsets[frame & 15];
     // All loads of the four rows first (normal, position, reprojection), then
     // the colours and the previous accumulation's taps.
-    f3 n[kSubs], pos[kSubs];
+    f3 n[kSubs], pos[kSubs], alb[kSubs];
     float2 pp[kSubs];
     long lin[kSubs];
     uint32_t bits[kSubs];
@@ -422,6 +424,7 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, NoisyInputs in, Ca
         n[s] = ld3(in.n_cur, lin[s]);
         pos[s] = ld3(in.p_cur, lin[s]);
         pp[s] = prev_pixel_out[lin[s]];
+        if (TONE) alb[s] = ld3(albedo, lin[s]);
     }
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {
@@ -443,9 +446,10 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, NoisyInputs in, Ca
             c.x = c.x < 0.f ? 0.f : c.x;
             c.y = c.y < 0.f ? 0.f : c.y;
             c.z = c.z < 0.f ? 0.f : c.z;
-            st3(acc_out, lin[s],
-                blend_filtered(P, c, pp[s].x, pp[s].y, (uint8_t)((bits[s] >> 1) & 15u), (uint8_t)(bits[s] >> 8),
-                               acc_prev, frame));
+            const f3 acc = blend_filtered(P, c, pp[s].x, pp[s].y, (uint8_t)((bits[s] >> 1) & 15u),
+                                          (uint8_t)(bits[s] >> 8), acc_prev, frame);
+            st3(acc_out, lin[s], acc);
+            if (TONE) st3(tone_out, lin[s], tone_map(alb[s], acc));  // bmfr.cl:851-856
         }
     }
 #ifdef BMFR_STAMPS
@@ -464,8 +468,13 @@ bool fused_supported(const Params& P) {
 
 template <int NS, int FS, bool HALF>
 static void launch_k1(const Params& P, hipStream_t st, const FusedArgs& A) {
-    hipLaunchKernelGGL((k_fused<NS, FS, HALF>), dim3(P.blocks_x * P.blocks_y), dim3(kThreads), 0, st, P, A.in,
-                       A.cam, A.frame, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out, A.acc_out,
+    if (k1_tone_maps(P))
+        hipLaunchKernelGGL((k_fused<NS, FS, HALF, true>), dim3(P.blocks_x * P.blocks_y), dim3(kThreads), 0, st, P,
+                           A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
+                           A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
+    else
+    hipLaunchKernelGGL((k_fused<NS, FS, HALF, false>), dim3(P.blocks_x * P.blocks_y), dim3(kThreads), 0, st, P, A.in,
+                       A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out, A.acc_out,
                        A.noise_table, A.stamps);
 }
 

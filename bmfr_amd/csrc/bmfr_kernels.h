@@ -543,15 +543,17 @@ __device__ __forceinline__ f3 tone_map(f3 albedo, f3 a) {
               fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.z * a.z), g), 0.f), 1.f)};
 }
 
-// TAA for one pixel (bmfr.cl:873-973); `tone(dx, dy)` returns the tone-mapped
-// colour of an in-image neighbour.
-template <class Tone>
-__device__ __forceinline__ f3 taa_pixel(const Params& P, int x, int y, f3 me, float2 pf,
-                                        const float* __restrict__ prev_frame, int frame, Tone tone) {
+// TAA for one pixel (bmfr.cl:873-973).  `ycocg(dx, dy)` returns
+// RGB_to_YCoCg of an in-image neighbour's tone-mapped colour (the centre's is
+// passed as me_y).
+template <class Ycocg>
+__device__ __forceinline__ f3 taa_pixel(const Params& P, int x, int y, f3 me, f3 me_y, float2 pf,
+                                        const float* __restrict__ prev_frame, int frame, Ycocg ycocg) {
     const int W = P.width, H = P.height;
     const float flx = floorf(pf.x), fly = floorf(pf.y);
+    if (frame == 0 || flx < -1.f || fly < -1.f || flx >= (float)W || fly >= (float)H)
+        return me;  // bmfr.cl:884-890 (compared as floats: no int overflow)
     const int ix = (int)flx, iy = (int)fly;
-    if (frame == 0 || ix < -1 || iy < -1 || ix >= W || iy >= H) return me;  // bmfr.cl:884-890
     f3 mnb{INFINITY, INFINITY, INFINITY}, mnc = mnb;
     f3 mxb{-INFINITY, -INFINITY, -INFINITY}, mxc = mxb;
 #pragma unroll
@@ -560,8 +562,7 @@ __device__ __forceinline__ f3 taa_pixel(const Params& P, int x, int y, f3 me, fl
         for (int dx = -1; dx < 2; ++dx) {  // bmfr.cl:897-920
             const int sx = x + dx, sy = y + dy;
             if (sx >= 0 && sy >= 0 && sx < W && sy < H) {
-                f3 s = (dx == 0 && dy == 0) ? me : tone(dx, dy);
-                s = rgb_to_ycocg(s);
+                const f3 s = (dx == 0 && dy == 0) ? me_y : ycocg(dx, dy);
                 if (dx == 0 || dy == 0) {
                     mnc = f3{fminf(mnc.x, s.x), fminf(mnc.y, s.y), fminf(mnc.z, s.z)};
                     mxc = f3{fmaxf(mxc.x, s.x), fmaxf(mxc.y, s.y), fmaxf(mxc.z, s.z)};
@@ -575,15 +576,20 @@ __device__ __forceinline__ f3 taa_pixel(const Params& P, int x, int y, f3 me, fl
     const float fx = pf.x - flx, fy = pf.y - fly;
     const float omx = 1.f - fx, omy = 1.f - fy;
     const float tw[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
+    f3 pc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // taps loaded up front (clamped address when skipped)
+        const int sx = min(max(ix + (i & 1), 0), W - 1), sy = min(max(iy + (i >> 1), 0), H - 1);
+        pc[i] = ld3(prev_frame, (long)sy * W + sx);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // bmfr.cl:929-960
         const bool okx = (i & 1) ? (ix < W - 1) : (ix >= 0);
         const bool oky = (i >> 1) ? (iy < H - 1) : (iy >= 0);
         if (okx && oky) {
-            const f3 pc = ld3(prev_frame, (long)(iy + (i >> 1)) * W + ix + (i & 1));
-            prev.x = prev.x + tw[i] * pc.x;
-            prev.y = prev.y + tw[i] * pc.y;
-            prev.z = prev.z + tw[i] * pc.z;
+            prev.x = prev.x + tw[i] * pc[i].x;
+            prev.y = prev.y + tw[i] * pc[i].y;
+            prev.z = prev.z + tw[i] * pc[i].z;
             total = total + tw[i];
         }
     }

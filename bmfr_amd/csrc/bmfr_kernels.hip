@@ -141,44 +141,53 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
     if (x >= P.width || y >= P.height) return;
     const long lin = (long)y * P.width + x;
-    const f3 r = taa_pixel(P, x, y, ld3(new_frame, lin), prev_pixel[lin], prev_frame, frame,
-                           [&](int dx, int dy) { return ld3(new_frame, lin + (long)dy * P.width + dx); });
+    const f3 me = ld3(new_frame, lin);
+    const f3 r = taa_pixel(P, x, y, me, rgb_to_ycocg(me), prev_pixel[lin], prev_frame, frame, [&](int dx, int dy) {
+        return rgb_to_ycocg(ld3(new_frame, lin + (long)dy * P.width + dx));
+    });
     st3(result, lin, r);
 }
 
-// ----------------------------------------------------- fused K2: tone + TAA --
-// One 64x16 tile per 256-thread work-group.  The tile and a 1-pixel halo are
-// tone-mapped from the accumulated filtered colour and the albedo straight
-// into LDS (the fused K1 never writes a tone-mapped frame), then TAA reads its
-// 3x3 neighbourhoods from LDS.
+// --------------------------------------------------------- fused K2: TAA --
+// One 64x16 tile per 256-thread work-group.  The tile's tone-mapped colours
+// and a 1-pixel halo go to LDS once, as RGB and as YCoCg, and the 3x3
+// neighbourhoods (bmfr.cl:897-920) are read from there.  TONE: the tile is
+// tone-mapped here from the accumulated colour and the albedo (K1 then
+// writes no tone-mapped frame); otherwise K1's tone-mapped frame is read.
 constexpr int kTaaW = 64, kTaaH = 16;
-__global__ __launch_bounds__(256) void k_tone_taa(Params P, const float* __restrict__ acc,
-                                                  const float* __restrict__ albedo,
-                                                  const float2* __restrict__ prev_pixel,
-                                                  float* __restrict__ result,
-                                                  const float* __restrict__ prev_frame, int frame) {
+template <bool TONE>
+__global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __restrict__ src,
+                                                   const float* __restrict__ albedo,
+                                                   const float2* __restrict__ prev_pixel,
+                                                   float* __restrict__ result,
+                                                   const float* __restrict__ prev_frame, int frame) {
     constexpr int HW = kTaaW + 2, HH = kTaaH + 2, N = HW * HH;
-    __shared__ float T[3][N];
+    constexpr int ITER = (N + 255) / 256;
+    __shared__ float T[3][N];  // RGB
+    __shared__ float Y[3][N];  // YCoCg
     const int t = threadIdx.x;
     const int x0 = blockIdx.x * kTaaW, y0 = blockIdx.y * kTaaH;
-    constexpr int ITER = (N + 255) / 256;
-    f3 al[ITER], ac[ITER];  // all tile loads in flight before any tone mapping
+    f3 v[ITER], al[ITER];
 #pragma unroll
-    for (int k = 0; k < ITER; ++k) {
+    for (int k = 0; k < ITER; ++k) {  // all tile loads in flight first
         const int i = t + 256 * k;
         const int x = min(max(x0 - 1 + i % HW, 0), P.width - 1), y = min(max(y0 - 1 + i / HW, 0), P.height - 1);
         const long lin = (long)y * P.width + x;
-        al[k] = ld3(albedo, lin);
-        ac[k] = ld3(acc, lin);
+        v[k] = ld3(src, lin);
+        if (TONE) al[k] = ld3(albedo, lin);
     }
 #pragma unroll
     for (int k = 0; k < ITER; ++k) {
         const int i = t + 256 * k;
-        if (i < N) {
-            const f3 c = tone_map(al[k], ac[k]);  // clamped halo pixels are never read
+        if (i < N) {  // clamped halo entries are never read
+            const f3 c = TONE ? tone_map(al[k], v[k]) : v[k];
+            const f3 yc = rgb_to_ycocg(c);
             T[0][i] = c.x;
             T[1][i] = c.y;
             T[2][i] = c.z;
+            Y[0][i] = yc.x;
+            Y[1][i] = yc.y;
+            Y[2][i] = yc.z;
         }
     }
     __syncthreads();
@@ -195,13 +204,13 @@ __global__ __launch_bounds__(256) void k_tone_taa(Params P, const float* __restr
         const int x = x0 + tx, y = y0 + ty;
         if (x < P.width && y < P.height) {
             const int c = (ty + 1) * HW + tx + 1;
-            const long lin = (long)y * P.width + x;
             const f3 me{T[0][c], T[1][c], T[2][c]};
-            const f3 r = taa_pixel(P, x, y, me, pf[k], prev_frame, frame, [&](int dx, int dy) {
+            const f3 me_y{Y[0][c], Y[1][c], Y[2][c]};
+            const f3 r = taa_pixel(P, x, y, me, me_y, pf[k], prev_frame, frame, [&](int dx, int dy) {
                 const int n = c + dy * HW + dx;
-                return f3{T[0][n], T[1][n], T[2][n]};
+                return f3{Y[0][n], Y[1][n], Y[2][n]};
             });
-            st3(result, lin, r);
+            st3(result, (long)y * P.width + x, r);
         }
     }
 }
@@ -366,8 +375,12 @@ hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& 
         if (e != hipSuccess) return e;
         if (mid) (void)hipEventRecord(mid, st);
         const dim3 grd((P.width + kTaaW - 1) / kTaaW, (P.height + kTaaH - 1) / kTaaH);
-        hipLaunchKernelGGL(k_tone_taa, grd, dim3(256), 0, st, P, A.acc_out, A.albedo, A.prev_pixel_out,
-                           A.result_out, A.result_prev, A.frame);
+        if (k1_tone_maps(P))
+            hipLaunchKernelGGL(k_fused_taa<false>, grd, dim3(256), 0, st, P, A.tone_out, A.albedo,
+                               A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
+        else
+            hipLaunchKernelGGL(k_fused_taa<true>, grd, dim3(256), 0, st, P, A.acc_out, A.albedo,
+                               A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
         return hipGetLastError();
     }
     if (P.not_scaled == 4 && P.scaled == 6) e = launch_fused_t<4, 6>(P, st, A);

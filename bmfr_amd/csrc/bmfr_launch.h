@@ -27,6 +27,11 @@ struct FusedArgs {
 
 bool fitter_supported(int not_scaled, int scaled);
 bool fused_supported(const Params& P);
+// Where the canonical path tone-maps (bmfr.cl:851-856): in K2 for each tile
+// pixel + halo (default: K1 is latency-bound and its VALU is the critical
+// resource; measured 0.68 vs 0.74 ms/frame at 4K), or in K1 for each owned
+// pixel, writing a tone-mapped frame (BMFR_FUSED_KERNEL=k1tone).
+inline bool k1_tone_maps(const Params& P) { return P.fused_variant == 2; }
 hipError_t launch_fused_k1(const Params& P, hipStream_t st, const FusedArgs& A);
 
 hipError_t launch_accumulate_noisy(const Params& P, hipStream_t st, float2* prev_pixel, uint8_t* accept,
