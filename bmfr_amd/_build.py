@@ -16,7 +16,7 @@ LIB = os.path.join(HERE, "libbmfr.so")
 DIAG_LIB = os.path.join(HERE, "libbmfr_diag.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["bmfr_kernels.hip", "bmfr_fused.hip", "bmfr_capi.hip", "bmfr_synth.hip"]
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize",
          "-Wall", "-Wno-unused-function"]
 
 
@@ -26,18 +26,22 @@ def _deps_mtime() -> float:
     return max(os.path.getmtime(f) for f in files)
 
 
-def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, diag: bool = False, variant: str = "",
+          extra_flags=()) -> str:
     """Build libbmfr.so (or, diag=True, libbmfr_diag.so: same library with
-    in-kernel phase timestamps compiled in, for profiling only)."""
-    lib = DIAG_LIB if diag else LIB
+    in-kernel phase timestamps compiled in, for profiling only; or, with
+    variant=NAME, libbmfr_NAME.so built with extra_flags, for A/B timing --
+    selected at run time by BMFR_LIB=NAME)."""
+    lib = DIAG_LIB if diag else (os.path.join(HERE, f"libbmfr_{variant}.so") if variant else LIB)
     if not force and os.path.exists(lib) and os.path.getmtime(lib) >= _deps_mtime():
         return lib
-    objdir = os.path.join(HERE, "_obj_diag" if diag else "_obj")
+    objdir = os.path.join(HERE, "_obj_diag" if diag else (f"_obj_{variant}" if variant else "_obj"))
     os.makedirs(objdir, exist_ok=True)
 
     def compile_one(src: str) -> str:
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
-        cmd = [HIPCC, *FLAGS, *(["-DBMFR_STAMPS"] if diag else []), "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [HIPCC, *FLAGS, *(["-DBMFR_STAMPS"] if diag else []), *extra_flags, "-c",
+               os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
@@ -52,5 +56,10 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
 
 
 if __name__ == "__main__":
-    import sys
-    print(build(force=True, verbose=True, diag="--diag" in sys.argv))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--diag", action="store_true")
+    ap.add_argument("--variant", default="")
+    ap.add_argument("--flags", default="", help="extra hipcc flags for a variant build")
+    a = ap.parse_args()
+    print(build(force=True, verbose=True, diag=a.diag, variant=a.variant, extra_flags=a.flags.split()))

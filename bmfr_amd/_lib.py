@@ -13,8 +13,10 @@ import os
 import torch  # noqa: F401  (see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# BMFR_LIB=diag selects the diagnostic build (in-kernel timestamps) for profiling.
-LIB_PATH = os.path.join(HERE, "libbmfr_diag.so" if os.environ.get("BMFR_LIB") == "diag" else "libbmfr.so")
+# BMFR_LIB=NAME selects libbmfr_NAME.so: the diagnostic build (diag, in-kernel
+# timestamps) or an A/B variant build (bmfr_amd/_build.py --variant).
+_variant = os.environ.get("BMFR_LIB", "")
+LIB_PATH = os.path.join(HERE, f"libbmfr_{_variant}.so" if _variant else "libbmfr.so")
 
 MAX_FEATURES = 16
 

@@ -296,8 +296,11 @@ __device__ __forceinline__ void back_substitute(K1Lds<B>& L, int t) {
     if (x < B - 3) L.weights[x * 3 + ch] = R[((RE - 1) * RE + x) * 3 + ch];
 }
 
+#ifndef BMFR_K1_WAVES
+#define BMFR_K1_WAVES 1  // minimum waves per SIMD requested from the register allocator
+#endif
 template <int NS, int FS, bool HALF, bool TONE>
-__global__ __launch_bounds__(kThreads) void k_fused(Params P, NoisyInputs in, Camera cam, int frame,
+__global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, NoisyInputs in, Camera cam, int frame,
                                                     const float* __restrict__ albedo,
                                                     float* __restrict__ tone_out,
                                                     const float* __restrict__ acc_prev,

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output for profiles/.
+
+  prof_summary.py stats <dir>          kernel_stats.csv -> markdown table
+  prof_summary.py pmc <dir> <counter>  counter_collection.csv -> per-kernel mean
+  prof_summary.py traffic <fetch_dir> <write_dir> <workload> <pixels> <alg_bytes_per_px>
+                                       -> profiles/pmc_k1.json entry (HBM bytes per K1 launch)
+
+FETCH_SIZE / WRITE_SIZE are KB per dispatch (rocprofv3 derived counters).
+MI355X_MICROARCH.md (HBM): on gfx950 FETCH_SIZE reads half the bytes of a
+wide coalesced stream, so the corrected read traffic is 2 x FETCH_SIZE; the
+raw value is kept beside it because our gathers are not all 16-B streams.
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+
+def find(d, pattern):
+    hits = glob.glob(os.path.join(d, "**", pattern), recursive=True)
+    if not hits:
+        sys.exit(f"no {pattern} under {d}")
+    return hits[0]
+
+
+def short(name):
+    n = name.split("(")[0]
+    for k in ("k_fused_taa", "k_fused", "k_noise_table", "k_synth", "k_tone_taa", "k_taa", "k_fitter",
+              "k_weighted_sum", "k_accumulate_filtered", "k_accumulate_noisy"):
+        if k in n:
+            return k + ("<tone>" if "k_fused_taa" in n and "ILb1E" in n else "")
+    return n[:60]
+
+
+def stats(d):
+    rows = list(csv.DictReader(open(find(d, "*kernel_stats.csv"))))
+    out = ["| kernel | calls | total ms | avg us | min us | max us | % |", "|---|---|---|---|---|---|---|"]
+    for r in rows:
+        out.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
+                   f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['MinNs']) / 1e3:.1f} | "
+                   f"{float(r['MaxNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} |")
+    return "\n".join(out)
+
+
+def pmc(d, counter):
+    rows = list(csv.DictReader(open(find(d, "*counter_collection.csv"))))
+    per = {}
+    for r in rows:
+        if r.get("Counter_Name", r.get("Counter-Name")) != counter:
+            continue
+        per.setdefault(short(r["Kernel_Name"]), []).append(float(r["Counter_Value"]))
+    return {k: statistics.mean(v) for k, v in per.items()}
+
+
+def main():
+    cmd = sys.argv[1]
+    if cmd == "stats":
+        print(stats(sys.argv[2]))
+    elif cmd == "pmc":
+        print(json.dumps(pmc(sys.argv[2], sys.argv[3]), indent=1))
+    elif cmd == "traffic":
+        fetch_dir, write_dir, workload, px, alg = sys.argv[2:7]
+        f = pmc(fetch_dir, "FETCH_SIZE")["k_fused"]
+        w = pmc(write_dir, "WRITE_SIZE")["k_fused"]
+        entry = {"fetch_kb_raw": f, "write_kb": w,
+                 "hbm_bytes_per_launch": (2 * f + w) * 1024,
+                 "hbm_bytes_per_launch_raw": (f + w) * 1024,
+                 "algorithmic_bytes_per_launch": int(px) * int(alg),
+                 "note": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE half-count correction, "
+                         "MI355X_MICROARCH.md HBM); raw = FETCH_SIZE + WRITE_SIZE"}
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_k1.json")
+        d = json.load(open(path)) if os.path.exists(path) else {}
+        d[workload] = entry
+        json.dump(d, open(path, "w"), indent=1)
+        print(json.dumps(entry, indent=1))
+
+
+if __name__ == "__main__":
+    main()
