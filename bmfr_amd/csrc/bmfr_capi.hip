@@ -103,9 +103,14 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     P.normal_limit_sq = as_kernel_literal(c->normal_limit_squared);
     P.half_tmp = c->use_half_precision_in_tmp_data ? 1 : 0;
     // Diagnostic A/B overrides of the fused path: BMFR_FUSED_KERNEL=block
-    // (generic-feature K1) or k1tone (tone mapping in K1 instead of K2).
+    // (generic-feature K1), k1tone (row-split K1 with tone mapping in K1) or
+    // rows (row-split K1, bmfr_fused.hip, instead of the column-split one).
     const char* v = std::getenv("BMFR_FUSED_KERNEL");
-    P.fused_variant = !v ? 0 : std::strcmp(v, "block") == 0 ? 1 : std::strcmp(v, "k1tone") == 0 ? 2 : 0;
+    P.fused_variant = !v                                ? 0
+                      : std::strcmp(v, "block") == 0   ? 1
+                      : std::strcmp(v, "k1tone") == 0  ? 2
+                      : std::strcmp(v, "rows") == 0    ? 3
+                                                       : 0;
     return P;
 }
 

@@ -1,0 +1,534 @@
+// bmfr_fused_cols.hip -- fused frame kernel K1, column-split form (default for
+// the canonical feature lists with half tmp_data).
+//
+// Same computation as k_fused (bmfr_fused.hip): accumulate_noisy_data ->
+// min/max scaling -> Householder QR -> back substitution -> weighted_sum ->
+// temporal blend (bmfr.cl:287-849), one 256-thread work-group per 32x32 block,
+// every value rounded exactly as upstream rounds it.  What differs is who
+// holds the design matrix during the fit:
+//
+//   * phase 1: thread (wave w, lane l) computes the features of rows
+//     r = l + 64 j, j = 4w..4w+3, and writes them to an LDS matrix;
+//   * fit: wave w takes COLUMNS c = w, w+4, w+8, ... -- all 1024 rows of each,
+//     lane l holding rows l + 64 j, j = 0..15 (8 packed-half registers per
+//     column).  Upstream's fitter work-item t = l + 64 m owns rows t + 256 s,
+//     i.e. j = m + 4 s, so each work-item partial and the first tree step
+//     (bmfr.cl:32-33) are in one lane and the rest of the tree runs on DPP /
+//     permlane swaps (bmfr_wave.h): every dot product, norm, min and max of
+//     the fit is a wave-local exact reduction, no LDS round trip, no barrier.
+//   * Householder step c needs only u_c, which the owner of column c publishes
+//     in LDS (double-buffered) as soon as it has applied step c-1 to that
+//     column, ahead of its other columns: one barrier per column instead of a
+//     block reduction per dot product.
+//   * phase 3 (weighted sum + blend) per pixel again, rows of phase 1.
+//
+// The R matrix, back substitution and phase-3 code are k_fused's.  Parity:
+// tests/test_gpu_parity.py (fused vs stage kernels bit for bit).
+#include <utility>
+
+#include "bmfr_launch.h"
+#include "bmfr_wave.h"
+
+namespace bmfr {
+namespace cols {
+
+constexpr int kThreads = 256;
+constexpr int kSlots = 16;    // rows per lane per column (row = lane + 64 j)
+constexpr int kUStride = 20;  // floats per lane in a u buffer: 16 + 4 (conflict-free 16-byte reads)
+
+template <int B>
+struct Lds {
+    union {
+        _Float16 M[B - 1][64 * kSlots];  // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
+        struct {
+            float u[2][64 * kUStride];  // Householder vectors, double-buffered by column parity
+            float keep[4][3][kThreads];  // phase 1 -> 3: previous accumulated filtered colour per item
+        };
+    };
+    float piv[2][2];                    // |u|^2 and RN(1/|u|^2) of the published vector
+    float R[(B - 2) * (B - 2) * 3];     // R[x][y][ch], x = column (as k_fused)
+    float weights[(B - 3) * 3];
+    float mm[3 * (B - 3)];              // per scaled feature: min, max, 1/(max-min)
+};
+static_assert(sizeof(float) * (2 * 64 * kUStride + 4 * 3 * kThreads) <= sizeof(_Float16) * 12 * 64 * kSlots,
+              "u buffers + phase-3 colours must fit in the matrix area (B >= 13)");
+
+template <int... I, class F>
+__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, I...>, F&& f) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    sfor_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+__device__ __forceinline__ float hget(const h2 (&a)[8], int j) { return (float)a[j >> 1][j & 1]; }
+
+__device__ __forceinline__ float lane_value(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// Sum over the wave of upstream work-item partials p[m] (work-item l + 64 m),
+// in upstream's association (bmfr.cl:25-44).
+template <RedOp OP>
+__device__ __forceinline__ float wave_reduce(const float (&p)[4]) {
+    return wave_tree<OP>(step2<OP>(p));
+}
+
+// Column update of Householder step c >= 1 (bmfr.cl:603-653) on one column:
+// dot with u over rows >= c, then A -= (2u) dot / |u|^2 on those rows.
+// With the fast path, the division is a Markstein step on the shared
+// reciprocal (exact for these operand ranges, tests/test_markstein.py);
+// non-finite or extreme operands take IEEE division (uniform branch).
+template <int c>
+__device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
+                                              int l) {
+    float x[kSlots];
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
+    float p[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        float s = 0.f;
+#pragma unroll
+        for (int si = 0; si < 4; ++si) {
+            const int j = m + 4 * si;
+            float pr = x[j] * u[j];
+            if (j == 0) pr = l >= c ? pr : 0.f;  // rows above the pivot: skipped (0.f + 0.f + ... is the same sum)
+            s = s + pr;
+        }
+        p[m] = s;
+    }
+    const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);  // (2u) dot == u (2 dot): same real product, one rounding
+    float nv[kSlots];
+    if (fabsf(c2) < 0x1p100f && ulen2 >= 0x1p-100f && ulen2 < 0x1p100f) {
+#pragma unroll
+        for (int j = 0; j < kSlots; ++j) nv[j] = x[j] - div_by_recip(u[j] * c2, ulen2, recip);
+    } else {
+        float c2s = c2;  // opaque: keeps the products inside this (cold) branch
+        asm volatile("" : "+v"(c2s));
+#pragma unroll
+        for (int j = 0; j < kSlots; ++j) {
+            nv[j] = x[j] - (u[j] * c2s) / ulen2;
+            __builtin_amdgcn_sched_barrier(0);  // never taken in practice: keep it narrow
+        }
+    }
+    nv[0] = l >= c ? nv[0] : x[0];
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) a[j >> 1][j & 1] = (_Float16)nv[j];
+    __builtin_amdgcn_sched_barrier(0);  // one column in flight: bounds the register footprint
+}
+
+// Step 0: column 0 is FEATURE_BUFFERS[0] = 1.f, so u = (1 - 32, 1, 1, ...),
+// |u|^2 = 1984 and u*x = x exactly (see k_fused's qr_column<0>).  Noise is
+// added to feature columns on this first load (bmfr.cl:625-627).
+template <bool NOISE>
+__device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const float* __restrict__ noise, double noise2) {
+    float x[kSlots];
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) {
+        x[j] = hget(a, j);
+        if (NOISE) x[j] = (float)((double)x[j] + noise2 * (double)noise[l + 64 * j]);
+    }
+    float p[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        float s = 0.f;
+#pragma unroll
+        for (int si = 0; si < 4; ++si) {
+            const int j = m + 4 * si;
+            s = s + (j == 0 && l == 0 ? x[0] * -31.f : x[j]);
+        }
+        p[m] = s;
+    }
+    const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);
+    constexpr float ulen2 = 1984.f;
+    const float recip = 1.f / ulen2;
+    float q, q0;
+    if (fabsf(c2) < 0x1p100f) {
+        q = div_by_recip(c2, ulen2, recip);
+        q0 = div_by_recip(-31.f * c2, ulen2, recip);
+    } else {
+        q = c2 / ulen2;
+        q0 = (-31.f * c2) / ulen2;
+    }
+    float nv[kSlots];
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) nv[j] = x[j] - q;
+    nv[0] = l == 0 ? x[0] - q0 : nv[0];
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) a[j >> 1][j & 1] = (_Float16)nv[j];
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// The owner of pivot column c (>= 1), once steps 0..c-1 are applied to it:
+// |x|^2 over rows >= c+1, the Householder vector u and |u|^2 (bmfr.cl:555-601),
+// published to LDS with the R column.
+template <int c, int B>
+__device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B>& L, int l) {
+    constexpr int RE = B - 2;
+    float x[kSlots];
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
+    float p[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        float s = 0.f;
+#pragma unroll
+        for (int si = 0; si < 4; ++si) {
+            const int j = m + 4 * si;
+            float pr = x[j] * x[j];
+            if (j == 0) pr = l >= c + 1 ? pr : 0.f;
+            s = s + pr;
+        }
+        p[m] = s;
+    }
+    const float sumsq = wave_reduce<RedOp::Sum>(p);
+    const float ucl = lane_value(x[0], c);  // u_vec[col]: row c is lane c, j = 0
+    const float vlen = sqrtf(sumsq + ucl * ucl);
+    const float ucl2 = ucl - vlen;
+    const float ulen2 = sumsq + ucl2 * ucl2;
+    if (l == c) x[0] = ucl2;
+    float4* dst = reinterpret_cast<float4*>(&L.u[c & 1][l * kUStride]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q] = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+    if (l == 0) {
+        L.piv[c & 1][0] = ulen2;
+        L.piv[c & 1][1] = 1.f / ulen2;
+    }
+    if (l < c) {  // R column: rows above the diagonal, then the diagonal
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) L.R[(c * RE + l) * 3 + ch] = x[0];
+    }
+    if (l == c) {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) L.R[(c * RE + c) * 3 + ch] = vlen;
+    }
+}
+
+// Wave W's part of the fit: columns c = W (mod 4), c >= 1 (column 0 is implicit).
+template <int W, int NS, int FS>
+struct WaveFit {
+    static constexpr int B = NS + FS + 3;
+    static constexpr int NF = B - 3;  // pivot columns
+    static constexpr int NSL = (B + 3) / 4;
+    static constexpr bool owns(int c) { return c >= 1 && c < B && (c & 3) == W; }
+
+    template <int c>
+    static __device__ __forceinline__ void step(h2 (&a)[NSL][8], Lds<B>& L, int l, const float* __restrict__ noise,
+                                                double noise2) {
+        constexpr int nxt = c + 1;
+        constexpr bool publish = nxt < NF && owns(nxt);
+        if constexpr (c == 0) {
+            if constexpr (publish) {
+                update_column0<(nxt < NF)>(a[nxt >> 2], l, noise + (nxt - 1) * kBlockPixels, noise2);
+                publish_pivot<nxt, B>(a[nxt >> 2], L, l);
+            }
+            sfor<NSL>([&](auto K) {
+                constexpr int fb = W + 4 * decltype(K)::value;
+                if constexpr (owns(fb) && !(publish && fb == nxt))
+                    update_column0<(fb < NF)>(a[fb >> 2], l, noise + (fb - 1) * kBlockPixels, noise2);
+            });
+        } else {
+            constexpr bool any = [] {
+                for (int fb = c + 1; fb < B; ++fb)
+                    if (owns(fb)) return true;
+                return false;
+            }();
+            if constexpr (any) {
+                float u[kSlots];
+                const float4* src = reinterpret_cast<const float4*>(&L.u[c & 1][l * kUStride]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = src[q];
+                    u[4 * q] = v.x;
+                    u[4 * q + 1] = v.y;
+                    u[4 * q + 2] = v.z;
+                    u[4 * q + 3] = v.w;
+                }
+                const float ulen2 = L.piv[c & 1][0], recip = L.piv[c & 1][1];
+                if constexpr (publish) {
+                    update_column<c>(a[nxt >> 2], u, ulen2, recip, l);
+                    publish_pivot<nxt, B>(a[nxt >> 2], L, l);
+                }
+                sfor<NSL>([&](auto K) {
+                    constexpr int fb = W + 4 * decltype(K)::value;
+                    if constexpr (owns(fb) && fb > c && !(publish && fb == nxt))
+                        update_column<c>(a[fb >> 2], u, ulen2, recip, l);
+                });
+            }
+        }
+        if constexpr (c + 1 < NF) __syncthreads();  // u_{c+1} published
+    }
+
+    template <int... C>
+    static __device__ __forceinline__ void steps(h2 (&a)[NSL][8], Lds<B>& L, int l, const float* __restrict__ noise,
+                                                 double noise2, std::integer_sequence<int, C...>) {
+        (step<C>(a, L, l, noise, noise2), ...);
+    }
+
+    // after_load(): runs once the matrix is in registers and the LDS area is free.
+    template <class AfterLoad>
+    static __device__ __forceinline__ void run(Lds<B>& L, int l, const float* __restrict__ noise, double noise2,
+                                               AfterLoad&& after_load) {
+        h2 a[NSL][8];
+        sfor<NSL>([&](auto K) {
+            constexpr int c = W + 4 * decltype(K)::value;
+            if constexpr (owns(c)) {
+                const uint4* src = reinterpret_cast<const uint4*>(&L.M[c - 1][l * kSlots]);
+                const uint4 lo = src[0], hi = src[1];
+                const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+                for (int i = 0; i < 8; ++i) a[c >> 2][i] = __builtin_bit_cast(h2, w[i]);
+            }
+        });
+        __syncthreads();  // the u buffers alias M
+        after_load();
+
+        // Scale the position features to the block's [min, max] (bmfr.cl:510-542).
+        sfor<NSL>([&](auto K) {
+            constexpr int c = W + 4 * decltype(K)::value;
+            if constexpr (owns(c) && c >= NS && c < NF) {
+                float hi[4], lo[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    hi[m] = -INFINITY;
+                    lo[m] = INFINITY;
+#pragma unroll
+                    for (int si = 0; si < 4; ++si) {
+                        const float v = hget(a[c >> 2], m + 4 * si);
+                        hi[m] = fmaxf(v, hi[m]);
+                        lo[m] = fminf(v, lo[m]);
+                    }
+                }
+                const float bmax = wave_reduce<RedOp::Max>(hi);
+                const float bmin = wave_reduce<RedOp::Min>(lo);
+                const float d = bmax - bmin;
+                const bool divide = fabsf(d) > 1.0f;  // scale(), bmfr.cl:200-205
+                const float rcp = 1.f / d;
+                if (l == 0) {
+                    L.mm[3 * (c - NS)] = bmin;
+                    L.mm[3 * (c - NS) + 1] = bmax;
+                    L.mm[3 * (c - NS) + 2] = rcp;
+                }
+#pragma unroll
+                for (int j = 0; j < kSlots; ++j) {
+                    const float v = hget(a[c >> 2], j) - bmin;
+                    a[c >> 2][j >> 1][j & 1] = (_Float16)(divide ? div_by_recip(v, d, rcp) : v);
+                }
+            }
+        });
+        if (W == 0 && l < 3) L.R[l] = 32.f;  // R(0,0) = |column 0|
+
+        steps(a, L, l, noise, noise2, std::make_integer_sequence<int, NF>{});
+
+        // Right-hand side: rows 0..B-4 of the colour columns (bmfr.cl:596-600).
+        sfor<NSL>([&](auto K) {
+            constexpr int c = W + 4 * decltype(K)::value;
+            if constexpr (owns(c) && c >= NF) {
+                if (l < NF) L.R[((B - 3) * (B - 2) + l) * 3 + (c - NF)] = hget(a[c >> 2], 0);
+            }
+        });
+    }
+};
+
+// Back substitution (bmfr.cl:658-699), as k_fused.
+template <int B>
+__device__ __forceinline__ void back_substitute(Lds<B>& L, int t) {
+    constexpr int RE = B - 2;
+    if (t >= 64) return;
+    const int ch = t % 3, x = t / 3;
+    float* R = L.R;
+    for (int i = RE - 2; i >= 0; --i) {
+        const float div = R[(i * RE + i) * 3 + ch];
+        __builtin_amdgcn_wave_barrier();
+        if (x < RE && x >= i) R[(x * RE + i) * 3 + ch] = R[(x * RE + i) * 3 + ch] / div;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (x == 0) {
+            float rhs = R[((RE - 1) * RE + i) * 3 + ch];
+            for (int j = i + 1; j < RE - 1; ++j) rhs = rhs - R[(j * RE + i) * 3 + ch];
+            R[((RE - 1) * RE + i) * 3 + ch] = rhs;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const float xi = R[((RE - 1) * RE + i) * 3 + ch];
+        if (x <= i && x < RE) R[(i * RE + x) * 3 + ch] = R[(i * RE + x) * 3 + ch] * xi;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (x < B - 3) L.weights[x * 3 + ch] = R[((RE - 1) * RE + x) * 3 + ch];
+}
+
+#ifndef BMFR_COLS_WAVES
+#define BMFR_COLS_WAVES 1  // minimum waves per SIMD requested from the register allocator
+#endif
+template <int NS, int FS>
+__global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params P, NoisyInputs in, Camera cam, int frame,
+                                                          const float* __restrict__ acc_prev,
+                                                          float* __restrict__ noisy_out,
+                                                          uint8_t* __restrict__ spp_out,
+                                                          float2* __restrict__ prev_pixel_out,
+                                                          float* __restrict__ acc_out,
+                                                          const float* __restrict__ noise,
+                                                          unsigned long long* __restrict__ stamps) {
+    constexpr int B = NS + FS + 3;
+    __shared__ Lds<B> L;
+    const int t = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int l = t & 63;
+    const int g = blockIdx.x;
+#ifdef BMFR_STAMPS
+#define BMFR_STAMP(k) \
+    if (t == 0 && stamps) stamps[(size_t)g * 8 + (k)] = __builtin_amdgcn_s_memtime()
+#else
+#define BMFR_STAMP(k) (void)stamps
+#endif
+    BMFR_STAMP(0);
+    const int bx = g % P.blocks_x, by = g / P.blocks_x;
+    const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
+
+    // ---- accumulate_noisy_data (bmfr.cl:310-484), rows l + 64 (4w + i) ----
+    h2 pk[B];  // features of an item pair, packed for one 4-byte LDS store per column
+    uint32_t spps = 0;   // per item i, bits 8i..8i+7: its new spp
+    uint32_t ibits = 0;  // per item i, bit i: owner; bit 4 + i: accepted taps with weight > 0
+    // The temporal part of accumulate_filtered_data is read at the noisy
+    // accumulation's taps (bmfr.cl:786-842) and parked in LDS for phase 3.
+    f3 keep_prev[4];
+#ifndef BMFR_P1_BATCH
+#define BMFR_P1_BATCH 2  // items whose current-frame loads are issued together (4: > 128 VGPRs)
+#endif
+    constexpr int PB = BMFR_P1_BATCH;
+#pragma unroll
+    for (int i0 = 0; i0 < 4; i0 += PB) {
+        NoisyCur cur[PB];
+#pragma unroll
+        for (int k = 0; k < PB; ++k)
+            cur[k] = noisy_load_current(P, in, bx * kEdge + lx, by * kEdge + ly + 2 * (i0 + k), frame);
+#pragma unroll
+        for (int k = 0; k < PB; ++k) {
+            const int i = i0 + k;
+            const NoisyItem it = noisy_item_spec<true>(P, in, cam, cur[k], frame, acc_prev);
+#pragma unroll
+            for (int f = 1; f < B; ++f) {
+                float v;
+                if (f < B - 3) v = feature_value(f, it.n, it.p);
+                else v = f == B - 3 ? it.color.x : (f == B - 2 ? it.color.y : it.color.z);
+                if (__builtin_isnan(v)) v = 0.0f;              // bmfr.cl:468-469
+                v = fmaxf(fminf(v, 65504.f), -65504.f);         // bmfr.cl:471-473
+                pk[f][i & 1] = (_Float16)v;
+            }
+            spps |= (uint32_t)it.spp << (8 * i);
+            ibits |= ((uint32_t)it.owner << i) | ((uint32_t)it.prev_f_divided << (4 + i));
+            keep_prev[i] = it.prev_f;
+            if (it.owner) {
+                st3(noisy_out, it.lin, it.color);
+                spp_out[it.lin] = it.spp;
+                prev_pixel_out[it.lin] = make_float2(it.pfx, it.pfy);
+            }
+            if (i & 1) {  // rows j = 4w + i - 1, 4w + i: adjacent halves of lane l's row slot
+#pragma unroll
+                for (int f = 1; f < B; ++f)
+                    *reinterpret_cast<uint32_t*>(&L.M[f - 1][l * kSlots + 4 * w + i - 1]) =
+                        __builtin_bit_cast(uint32_t, pk[f]);
+            }
+#ifdef BMFR_P1_SERIAL
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+    }
+    __syncthreads();
+    BMFR_STAMP(1);
+    BMFR_STAMP(2);  // scaling runs inside the per-wave fit
+
+    // ---- fit: min/max scaling, Householder QR, right-hand side ----
+    const auto park = [&] {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            L.keep[i][0][t] = keep_prev[i].x;
+            L.keep[i][1][t] = keep_prev[i].y;
+            L.keep[i][2][t] = keep_prev[i].z;
+        }
+    };
+    switch (w) {
+        case 0: WaveFit<0, NS, FS>::run(L, l, noise, P.noise2, park); break;
+        case 1: WaveFit<1, NS, FS>::run(L, l, noise, P.noise2, park); break;
+        case 2: WaveFit<2, NS, FS>::run(L, l, noise, P.noise2, park); break;
+        default: WaveFit<3, NS, FS>::run(L, l, noise, P.noise2, park); break;
+    }
+    __syncthreads();
+    BMFR_STAMP(3);
+    back_substitute<B>(L, t);
+    __syncthreads();
+    BMFR_STAMP(4);
+
+    // ---- weighted_sum (bmfr.cl:717-750) + temporal blend (bmfr.cl:778-849) ----
+    int l3 = l;  // opaque copy: recompute phase-1 addresses instead of keeping them live across the fit
+    asm volatile("" : "+v"(l3));
+    const int2 off = kBlockOffsets[frame & 15];
+    long lin[4];
+    f3 nrm[4], wp[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int px = bx * kEdge + (l3 & (kEdge - 1)) - kEdge / 2 + off.x;
+        const int py = by * kEdge + (l3 >> 5) + 8 * w + 2 * i - kEdge / 2 + off.y;
+        lin[i] = (ibits & (1u << i)) ? (long)py * P.width + px : 0;  // margins: a valid pixel, skipped below
+        nrm[i] = ld3(in.n_cur, lin[i]);
+        wp[i] = ld3(in.p_cur, lin[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (ibits & (1u << i)) {
+            f3 c{0.f, 0.f, 0.f};
+#pragma unroll
+            for (int f = 0; f < B - 3; ++f) {
+                float v = feature_value(f, nrm[i], wp[i]);
+                if (f >= NS) {
+                    const float bmin = L.mm[3 * (f - NS)], bmax = L.mm[3 * (f - NS) + 1];
+                    const float d = bmax - bmin;
+                    v = v - bmin;
+                    if (fabsf(d) > 1.0f) v = div_by_recip(v, d, L.mm[3 * (f - NS) + 2]);
+                }
+                c.x = c.x + L.weights[3 * f] * v;
+                c.y = c.y + L.weights[3 * f + 1] * v;
+                c.z = c.z + L.weights[3 * f + 2] * v;
+            }
+            c.x = c.x < 0.f ? 0.f : c.x;
+            c.y = c.y < 0.f ? 0.f : c.y;
+            c.z = c.z < 0.f ? 0.f : c.z;
+            // bmfr.cl:834-849: alpha from the current spp when the taps carried weight
+            const float alpha = (ibits & (1u << (4 + i)))
+                                    ? fmaxf(1.f / (float)((spps >> (8 * i)) & 255u), P.second_blend_alpha)
+                                    : 1.f;
+            const float beta = 1.f - alpha;
+            const int t3 = l3 + 64 * w;
+            const f3 prev{L.keep[i][0][t3], L.keep[i][1][t3], L.keep[i][2][t3]};
+            const f3 acc{alpha * c.x + beta * prev.x, alpha * c.y + beta * prev.y, alpha * c.z + beta * prev.z};
+            st3(acc_out, lin[i], acc);
+        }
+    }
+#ifdef BMFR_STAMPS
+    __syncthreads();
+#endif
+    BMFR_STAMP(5);
+#undef BMFR_STAMP
+}
+
+}  // namespace cols
+
+bool fused_cols_supported(const Params& P) {
+    return P.half_tmp && P.fused_variant == 0 && fused_supported(P);
+}
+
+hipError_t launch_fused_k1_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
+    const dim3 grid(P.blocks_x * P.blocks_y), block(cols::kThreads);
+    if (P.scaled == 6)
+        hipLaunchKernelGGL((cols::k_fused_cols<4, 6>), grid, block, 0, st, P, A.in, A.cam, A.frame, A.acc_prev,
+                           A.noisy_out, A.spp_out, A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
+    else
+        hipLaunchKernelGGL((cols::k_fused_cols<4, 9>), grid, block, 0, st, P, A.in, A.cam, A.frame, A.acc_prev,
+                           A.noisy_out, A.spp_out, A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
+    return hipGetLastError();
+}
+
+}  // namespace bmfr

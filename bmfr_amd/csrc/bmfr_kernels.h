@@ -83,6 +83,13 @@ struct NoisyItem {
     uint8_t accept;
     uint8_t spp;
     bool owner;       // pixel_without_mirror inside the image
+    // noisy_item_spec<true> only: the previous accumulated filtered colour
+    // at the same taps, blended as accumulate_filtered_data does
+    // (bmfr.cl:786-842) -- prev_f (divided by the tap weight sum when > 0)
+    // and alpha_f, so acc = alpha_f * filtered + (1 - alpha_f) * prev_f.
+    f3 prev_f;
+    float alpha_f;
+    bool prev_f_divided;  // the tap weights summed to > 0 (alpha_f from spp)
 };
 
 struct NoisyInputs {
@@ -210,8 +217,10 @@ __device__ __forceinline__ NoisyCur noisy_load_current(const Params& P, const No
     return c;
 }
 
+template <bool FILT = false>
 __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const NoisyInputs& in, const Camera& cam,
-                                                     const NoisyCur& c, int frame) {
+                                                     const NoisyCur& c, int frame,
+                                                     const float* __restrict__ acc_prev = nullptr) {
     NoisyItem o;
     o.owner = c.owner;
     o.lin = (long)c.py * P.width + c.px;
@@ -223,6 +232,10 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
     float alpha = 1.f;
     f3 prev{0.f, 0.f, 0.f};
     float sample_spp = 0.f;
+    o.prev_f = f3{0.f, 0.f, 0.f};
+    o.alpha_f = 1.f;
+    o.prev_f_divided = false;
+    float tap_total = 0.f;
     if (frame > 0) {
         const float* M = cam.m;
         float u = dot4(M[0], M[4], M[8], M[12], wp.x, wp.y, wp.z, 1.f);
@@ -244,7 +257,7 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
         const float fx = pfx - flx, fy = pfy - fly;
         const float omx = 1.f - fx, omy = 1.f - fy;
         const float wts[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
-        f3 pp[4], pn[4], pc[4];
+        f3 pp[4], pn[4], pc[4], pa[4];
         float sp[4];
         bool inb[4];
 #pragma unroll
@@ -256,6 +269,7 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
             pn[i] = ld3(in.n_prev, s);
             pc[i] = ld3(in.noisy_prev, s);
             sp[i] = (float)in.spp_prev[s];
+            if (FILT) pa[i] = ld3(acc_prev, s);  // same taps (bmfr.cl:801-832)
         }
         float total = 0.f;
 #pragma unroll
@@ -269,6 +283,11 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
                 prev.y = prev.y + wts[i] * pc[i].y;
                 prev.z = prev.z + wts[i] * pc[i].z;
                 total = total + wts[i];
+                if (FILT) {  // accumulate_filtered_data's sums: same weights, same order
+                    o.prev_f.x = o.prev_f.x + wts[i] * pa[i].x;
+                    o.prev_f.y = o.prev_f.y + wts[i] * pa[i].y;
+                    o.prev_f.z = o.prev_f.z + wts[i] * pa[i].z;
+                }
             }
         }
         if (total > 0.f) {  // bmfr.cl:421-429
@@ -280,9 +299,18 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
             alpha = 1.f / (sample_spp + 1.f);
             alpha = fmaxf(alpha, P.blend_alpha);
         }
+        tap_total = total;
     }
     uint8_t new_spp = 1;  // bmfr.cl:433-442
     if (alpha < 1.f) new_spp = sample_spp > 254.f ? 255 : (uint8_t)((int)rintf(sample_spp) + 1);
+    if (FILT && tap_total > 0.f) {  // bmfr.cl:834-842 (the same sum of accepted tap weights)
+        const float rt = 1.f / tap_total;
+        o.prev_f_divided = true;
+        o.alpha_f = fmaxf(1.f / (float)new_spp, P.second_blend_alpha);
+        o.prev_f.x = div_shared(o.prev_f.x, tap_total, rt);
+        o.prev_f.y = div_shared(o.prev_f.y, tap_total, rt);
+        o.prev_f.z = div_shared(o.prev_f.z, tap_total, rt);
+    }
     const float beta = 1.f - alpha;
     o.color = f3{alpha * cur.x + beta * prev.x, alpha * cur.y + beta * prev.y, alpha * cur.z + beta * prev.z};
     o.pfx = pfx;

@@ -371,7 +371,7 @@ hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& 
         const int n = (P.buffers - 4) * kBlockPixels;
         hipLaunchKernelGGL(k_noise_table, dim3((n + 255) / 256), dim3(256), 0, st, A.frame, P.buffers,
                            A.noise_table);
-        e = launch_fused_k1(P, st, A);
+        e = fused_cols_supported(P) ? launch_fused_k1_cols(P, st, A) : launch_fused_k1(P, st, A);
         if (e != hipSuccess) return e;
         if (mid) (void)hipEventRecord(mid, st);
         const dim3 grd((P.width + kTaaW - 1) / kTaaW, (P.height + kTaaH - 1) / kTaaH);

@@ -33,6 +33,9 @@ bool fused_supported(const Params& P);
 // pixel, writing a tone-mapped frame (BMFR_FUSED_KERNEL=k1tone).
 inline bool k1_tone_maps(const Params& P) { return P.fused_variant == 2; }
 hipError_t launch_fused_k1(const Params& P, hipStream_t st, const FusedArgs& A);
+// Column-split K1 (bmfr_fused_cols.hip): default for half tmp_data.
+bool fused_cols_supported(const Params& P);
+hipError_t launch_fused_k1_cols(const Params& P, hipStream_t st, const FusedArgs& A);
 
 hipError_t launch_accumulate_noisy(const Params& P, hipStream_t st, float2* prev_pixel, uint8_t* accept,
                                    const NoisyInputs& in, float* noisy_out, uint8_t* spp_cur, void* tmp,

@@ -35,7 +35,7 @@ struct Params {
     float blend_alpha, second_blend_alpha, taa_blend_alpha;
     float position_limit_sq, normal_limit_sq;
     int half_tmp;                 // USE_HALF_PRECISION_IN_TMP_DATA
-    int fused_variant;            // 0 = default, 1 = generic-feature K1, 2 = tone map in K1 (A/B diagnostics)
+    int fused_variant;            // 0 = default, 1 = generic-feature K1, 2 = tone map in K1, 3 = row-split K1 (A/B diagnostics)
 };
 
 }  // namespace bmfr

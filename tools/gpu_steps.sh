@@ -1,9 +1,9 @@
 #!/bin/bash
 # Run a list of GPU steps on the gpurun box, each under its own time limit.
 # Usage: tools/gpu_steps.sh "<secs>:<name>:<command>" ...
-# A step's output goes to gpurun_out/<name>.log.  A plain failure (exit 1,
-# e.g. a failing test) lets the next step run; a crash / abort / timeout /
-# kill (124, 134, 137, 139 or > 128) ends the script there.
+# A step's output goes to gpurun_out/<name>.log.  Any failing step ends the
+# script there (a failure may be a GPU fault: nothing else runs on the GPU
+# after it).
 mkdir -p gpurun_out
 for step in "$@"; do
     secs="${step%%:*}"; rest="${step#*:}"
@@ -13,7 +13,7 @@ for step in "$@"; do
     rc=$?
     echo "=== [$name] exit $rc"
     tail -n 25 "gpurun_out/$name.log"
-    if [ $rc -ge 124 ]; then
+    if [ $rc -ne 0 ]; then
         echo "=== stopping: step $name ended with $rc"
         exit $rc
     fi

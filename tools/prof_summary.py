@@ -3,6 +3,7 @@
 
   prof_summary.py stats <dir>          kernel_stats.csv -> markdown table
   prof_summary.py pmc <dir> <counter>  counter_collection.csv -> per-kernel mean
+  prof_summary.py calib <dir> <counter> <bytes>   counter / true bytes per calibration kernel
   prof_summary.py traffic <fetch_dir> <write_dir> <workload> <pixels> <alg_bytes_per_px>
                                        -> profiles/pmc_k1.json entry (HBM bytes per K1 launch)
 
@@ -27,12 +28,11 @@ def find(d, pattern):
 
 
 def short(name):
-    n = name.split("(")[0]
-    for k in ("k_fused_taa", "k_fused", "k_noise_table", "k_synth", "k_tone_taa", "k_taa", "k_fitter",
-              "k_weighted_sum", "k_accumulate_filtered", "k_accumulate_noisy"):
-        if k in n:
-            return k + ("<tone>" if "k_fused_taa" in n and "ILb1E" in n else "")
-    return n[:60]
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    n = n.split("(")[0]
+    for ns in ("bmfr::cols::", "bmfr::"):
+        n = n.replace(ns, "")
+    return n[:70]
 
 
 def stats(d):
@@ -61,10 +61,15 @@ def main():
         print(stats(sys.argv[2]))
     elif cmd == "pmc":
         print(json.dumps(pmc(sys.argv[2], sys.argv[3]), indent=1))
+    elif cmd == "calib":
+        true_kb = int(sys.argv[4]) / 1024
+        for k, v in pmc(sys.argv[2], sys.argv[3]).items():
+            print(f"{k:40s} {sys.argv[3]} {v:12.0f} KB  counted/true {v / true_kb:.3f}")
     elif cmd == "traffic":
         fetch_dir, write_dir, workload, px, alg = sys.argv[2:7]
-        f = pmc(fetch_dir, "FETCH_SIZE")["k_fused"]
-        w = pmc(write_dir, "WRITE_SIZE")["k_fused"]
+        k1 = os.environ.get("K1_NAME", "k_fused_cols<4, 6>")
+        f = pmc(fetch_dir, "FETCH_SIZE")[k1]
+        w = pmc(write_dir, "WRITE_SIZE")[k1]
         entry = {"fetch_kb_raw": f, "write_kb": w,
                  "hbm_bytes_per_launch": (2 * f + w) * 1024,
                  "hbm_bytes_per_launch_raw": (f + w) * 1024,
