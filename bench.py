@@ -11,9 +11,14 @@ Workload at N=1: 3840x2160, reference default parameters (B = 13 features,
 half tmp_data, 32x32 blocks), frames W..W+K-1 of the sequence (temporal path
 active on every timed frame).
 
-Multi-GPU (torchrun, one process per GPU): weak scaling, each rank
-denoises its own 3840x2160 sequence; no data-path collective (see DESIGN.md
-"Multi-GPU").  Timing: barrier + synchronize around K frames, max over ranks.
+Multi-GPU (torchrun, one process per GPU): the frame is cut into a tile grid
+(1x1, 2x1, 2x2, 4x2), one tile per rank, and each rank denoises its tile
+with a tiled context; before every frame the ranks exchange the halo ring
+of the previous frame's temporal state over RCCL (bmfr_amd/tiling.py,
+DESIGN.md "Multi-GPU").  Default --scaling weak: every rank's tile is
+--width x --height (3840x2160), so 4 GPUs run a 7680x4320 frame; --scaling
+strong splits one --width x --height frame.  Timing: barrier + synchronize
+around K frames (exchange included), max over ranks.
 
 Extra JSON fields: `roofline` for the dominant kernel (K1), measured with HIP
 events on the stream it runs on; `cpu_baseline` = the CPU oracle
@@ -35,6 +40,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import bmfr_amd  # noqa: E402
+from bmfr_amd import tiling  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # Algorithmic bytes per pixel (SURVEY.md §8d, 18*s + 74 with s = 4 for f32 planes),
@@ -58,6 +64,9 @@ def parse():
     ap.add_argument("--third-order", action="store_true", help="B = 16 feature set (BASELINE config 5)")
     ap.add_argument("--cpu-frames", type=int, default=2, help="timed CPU-oracle frames (0 = skip)")
     ap.add_argument("--seed", type=int, default=0x424D4652)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="multi-GPU: weak = one --width x --height tile per GPU, strong = one frame split")
+    ap.add_argument("--halo", type=int, default=64, help="tile halo in pixels (>= 34 + max motion)")
     return ap.parse_args()
 
 
@@ -108,29 +117,48 @@ def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BMFR_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
+    # on one GPU (messages staged through host memory); default RCCL.
+    backend = os.environ.get("BMFR_DIST_BACKEND", "nccl")
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
-    W, H = a.width, a.height
+    tx, ty = tiling.grid_for(world)
+    if a.scaling == "weak":
+        W, H = a.width * tx, a.height * ty
+    else:
+        W, H = a.width, a.height
+    grid = tiling.TileGrid(W, H, tx, ty, halo=a.halo) if world > 1 else None
     scaled = bmfr_amd.SCALED_THIRD_ORDER if a.third_order else bmfr_amd.SCALED_DEFAULT
     cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, scaled=scaled,
-                              use_half_precision_in_tmp_data=a.half_tmp)
+                              use_half_precision_in_tmp_data=a.half_tmp,
+                              tile=grid.tile(rank) if grid else None, tile_halo=a.halo if grid else 0)
     den = bmfr_amd.Denoiser(cfg, device=local)
+    region = den.region
+    tile = grid.tile(rank) if grid else (0, 0, W, H)
     nfr = a.warmup + a.steps
-    seed = a.seed + rank  # each rank its own sequence (weak scaling)
+    seed = a.seed
 
-    # Render every frame into HBM up front (untimed).
-    frames = [bmfr_amd.synth_frame_device(W, H, f, seed=seed, device=local) for f in range(nfr)]
+    # Render every frame's region into HBM up front (untimed).
+    frames = [bmfr_amd.synth_region_device(W, H, region, f, seed=seed, device=local) for f in range(nfr)]
     cams = []
     for f in range(nfr):
         vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
         _, jit = bmfr_amd.synth_camera(W, H, f)
         cams.append((vp, jit))
+    transport = tiling.DistTransport(grid, rank, dev, host_staging=backend != "nccl") if grid else None
+    copier = tiling.HipCopier() if grid else None
     torch.cuda.synchronize()
 
     def run(f):
+        if transport is not None and f > 0:
+            transport.exchange(tiling.state_planes(den), copier)
         fr = frames[f]
         prev = frames[f - 1] if f > 0 else None
         den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], cams[f][0], cams[f][1], f,
@@ -153,7 +181,7 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = den.profile()
     if world > 1:
-        t = torch.tensor([elapsed], device="cuda")
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -161,20 +189,25 @@ def main():
     k1_ms = float(np.mean([p[1] for p in prof]))
     k2_ms = float(np.mean([p[2] for p in prof]))
     dev_ms = float(np.mean([p[3] for p in prof]))
-    px = W * H
+    tile_px = tile[2] * tile[3]
     workload = f"bmfr_{W}x{H}_B{cfg.buffer_count}_{'half' if a.half_tmp else 'f32'}tmp"
 
-    # Quality: PSNR of the last output against the clean render of that frame.
-    clean = bmfr_amd.synth_frame_device(W, H, nfr - 1, seed=seed, device=local, clean=True)["clean"]
-    out = den.copy_output(torch.empty(px * 3, device="cuda"))
+    # Quality: PSNR of this rank's tile of the last output against the clean render.
+    clean = bmfr_amd.synth_region_device(W, H, region, nfr - 1, seed=seed, device=local, clean=True)["clean"]
+    out = den.copy_output(torch.empty(region[2] * region[3] * 3, device=dev))
     torch.cuda.synchronize()
-    q = psnr(out.cpu().numpy(), clean.cpu().numpy())
-    noisy_tm = torch.clamp(torch.clamp(frames[nfr - 1]["albedo"] * frames[nfr - 1]["noisy"], min=0) ** 0.454545,
-                           0, 1)
-    q_in = psnr(noisy_tm.cpu().numpy(), clean.cpu().numpy())
+
+    def tile_of(x):
+        x = x.view(region[3], region[2], 3)
+        return x[tile[1] - region[1]:tile[1] - region[1] + tile[3], tile[0] - region[0]:tile[0] - region[0] + tile[2]]
+
+    q = psnr(tile_of(out).cpu().numpy(), tile_of(clean).cpu().numpy())
+    last = frames[nfr - 1]
+    noisy_tm = torch.clamp(torch.clamp(last["albedo"] * last["noisy"], min=0) ** 0.454545, 0, 1)
+    q_in = psnr(tile_of(noisy_tm).cpu().numpy(), tile_of(clean).cpu().numpy())
 
     if rank == 0:
-        achieved = K1_BYTES_PER_PX * px / (k1_ms * 1e-3) / 1e9
+        achieved = K1_BYTES_PER_PX * tile_px / (k1_ms * 1e-3) / 1e9
         line = {
             "metric": "ms/frame @1080p & 4K, 1/2/4/8 GPU; PSNR vs 4096spp reference",
             "value": round(ms_per_frame, 4),
@@ -184,22 +217,23 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_frame, 4),
             "higher_is_better": False,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": "f32" + ("+f16 tmp_data" if a.half_tmp else ""),
             "data": "synthetic (GPU-rendered 1-spp frames + features, resident in HBM)",
             "config": {"workload": workload, "image": f"{W}x{H}", "buffer_count": cfg.buffer_count,
                        "half_tmp_data": a.half_tmp, "frames_timed": a.steps,
-                       "parallelism": f"replica x{world}" if world > 1 else "single GPU"},
+                       "parallelism": f"tiles {tx}x{ty}, halo {a.halo} px, RCCL halo exchange" if world > 1
+                       else "single GPU"},
             "device_ms_per_frame": round(dev_ms, 4),
             "kernel_ms": {"fused_block_k1": round(k1_ms, 4), "taa_k2": round(k2_ms, 4)},
             "psnr_db": {"output": round(q, 2), "noisy_input": round(q_in, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(workload),
-                         "kernel": "k_fused_block (K1)",
-                         "algorithmic_bytes_per_launch": K1_BYTES_PER_PX * px,
-                         "frame_frac": round(FRAME_BYTES_PER_PX * px / (ms_per_frame * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                             4)},
+                         "kernel": "k_fused_cols (K1)" if a.half_tmp else "k_fused (K1)",
+                         "algorithmic_bytes_per_launch": K1_BYTES_PER_PX * tile_px,
+                         "frame_frac": round(FRAME_BYTES_PER_PX * W * H / (ms_per_frame * 1e-3) / 1e9
+                                             / (HBM_PEAK_GBS * world), 4)},
         }
         if world == 1 and a.cpu_frames > 0:
             line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_frames, seed)

@@ -47,6 +47,7 @@ class Config(C.Structure):
         ("position_limit_squared", C.c_double), ("normal_limit_squared", C.c_double),
         ("use_half_precision_in_tmp_data", C.c_int),
         ("tile_x", C.c_int), ("tile_y", C.c_int), ("tile_width", C.c_int), ("tile_height", C.c_int),
+        ("tile_halo", C.c_int),
     ]
 
 
@@ -58,6 +59,8 @@ class Sizes(C.Structure):
         ("blocks", C.c_int),
         ("tmp_data_bytes", C.c_size_t), ("weights_bytes", C.c_size_t),
         ("mins_maxs_bytes", C.c_size_t), ("image_bytes", C.c_size_t),
+        ("region_x", C.c_int), ("region_y", C.c_int), ("region_width", C.c_int), ("region_height", C.c_int),
+        ("region_bytes", C.c_size_t),
     ]
 
 
@@ -102,6 +105,7 @@ SIGNATURES = {
     "bmfr_debug_stamps": (_I, [_P, _P, C.c_size_t]),  # include/bmfr_debug.h
     "bmfr_synth_frame_host": (_I, [_I, _I, _I, C.c_uint32, _P, _P, _P, _P, _P]),
     "bmfr_synth_frame_device": (_I, [_I, _I, _I, C.c_uint32, _P, _P, _P, _P, _P, _P]),
+    "bmfr_synth_region_device": (_I, [_I, _I, _I, _I, _I, _I, _I, C.c_uint32, _P, _P, _P, _P, _P, _P]),
 }
 
 _lib = None

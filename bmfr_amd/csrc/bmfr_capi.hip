@@ -5,6 +5,7 @@
 // (bmfr.cpp:315-347), kernel argument binding (bmfr.cpp:349-383, 429-476) and
 // the Double_buffer swap (bmfr.cpp:122-135, 482-484).  No allocation happens
 // on the per-frame path; every call returns a status code.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -27,7 +28,7 @@ struct bmfr_ctx {
     float* result[2] = {nullptr, nullptr};
     float* tone = nullptr;
     float2* prev_pixel = nullptr;
-    float* noise_table = nullptr;
+    double* noise_table = nullptr;
     unsigned long long* stamps = nullptr;  // diagnostic: BMFR_STAMPS=1 with libbmfr_diag.so
     int cur = 0;
     bool has_frame = false;
@@ -58,6 +59,10 @@ float as_kernel_literal(double v) {
     return (float)std::strtod(buf, nullptr);
 }
 
+// Blocks reach 32 px past the tile (K2 needs the tile + 1 px), their
+// reprojection taps one more, TAA's bilinear taps one more.
+constexpr int kMinTileHalo = 34;
+
 bmfr_status validate(const bmfr_config* c) {
     if (!c) return BMFR_ERROR_INVALID_ARGUMENT;
     // mirror() is only valid less than one image size out of range
@@ -77,9 +82,16 @@ bmfr_status validate(const bmfr_config* c) {
     for (int i = 0; i < c->features_not_scaled + c->features_scaled; ++i)
         if (c->feature_buffers[i] < 0 || c->feature_buffers[i] >= BMFR_FEATURE_COUNT_)
             return BMFR_ERROR_INVALID_ARGUMENT;
-    if (c->tile_x || c->tile_y || c->tile_width || c->tile_height) return BMFR_ERROR_UNSUPPORTED;
+    if (c->tile_x || c->tile_y || c->tile_width || c->tile_height || c->tile_halo) {
+        if (c->tile_x < 0 || c->tile_y < 0 || c->tile_width <= 0 || c->tile_height <= 0 ||
+            c->tile_x + c->tile_width > c->image_width || c->tile_y + c->tile_height > c->image_height ||
+            c->tile_halo < kMinTileHalo)
+            return BMFR_ERROR_INVALID_ARGUMENT;
+    }
     return BMFR_OK;
 }
+
+bool is_tiled(const bmfr_config* c) { return c->tile_width > 0; }
 
 Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     Params P{};
@@ -111,6 +123,50 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
                       : std::strcmp(v, "k1tone") == 0  ? 2
                       : std::strcmp(v, "rows") == 0    ? 3
                                                        : 0;
+    P.ox = s->region_x;
+    P.oy = s->region_y;
+    P.stride = s->region_width;
+    P.rows = s->region_height;
+    // whole-grid launch (stage kernels, untiled frames)
+    P.bx0 = P.by0 = 0;
+    P.nbx = P.blocks_x;
+    P.nby = P.blocks_y;
+    P.tx0 = P.ty0 = 0;
+    P.tx1 = P.width;
+    P.ty1 = P.height;
+    return P;
+}
+
+// The launch parameters of frame `frame` for a tiled context: the blocks of
+// that frame's shifted grid (bmfr.cl:267-285, 310-317) that cover the tile
+// plus one pixel (TAA's 3x3), and the tile as K2's output.  Blocks without a
+// pixel inside the frame own nothing and are skipped.
+Params frame_params(const bmfr_ctx* c, int frame) {
+    Params P = c->P;
+    if (!is_tiled(&c->cfg)) return P;
+    const bmfr_config& g = c->cfg;
+    const int E = BMFR_BLOCK_EDGE_LENGTH;
+    const int ox = bmfr::kBlockOffsetTable[frame & 15][0], oy = bmfr::kBlockOffsetTable[frame & 15][1];
+    auto range = [&](int lo, int hi, int off, int nblocks, int& b0, int& nb) {
+        // block b covers pixels [E b - E/2 + off, E b + E/2 + off)
+        b0 = -1;
+        nb = 0;
+        for (int b = 0; b < nblocks; ++b) {
+            const int p0 = E * b - E / 2 + off, p1 = p0 + E;
+            if (p0 < hi && p1 > lo) {
+                if (b0 < 0) b0 = b;
+                nb = b - b0 + 1;
+            }
+        }
+    };
+    range(std::max(0, g.tile_x - 1), std::min(g.image_width, g.tile_x + g.tile_width + 1), ox, P.blocks_x, P.bx0,
+          P.nbx);
+    range(std::max(0, g.tile_y - 1), std::min(g.image_height, g.tile_y + g.tile_height + 1), oy, P.blocks_y,
+          P.by0, P.nby);
+    P.tx0 = g.tile_x;
+    P.ty0 = g.tile_y;
+    P.tx1 = g.tile_x + g.tile_width;
+    P.ty1 = g.tile_y + g.tile_height;
     return P;
 }
 
@@ -167,6 +223,17 @@ bmfr_status bmfr_config_sizes(const bmfr_config* c, bmfr_sizes* s) {
     s->weights_bytes = (size_t)s->blocks * (s->buffer_count - 3) * 3 * sizeof(float);
     s->mins_maxs_bytes = (size_t)s->blocks * c->features_scaled * 2 * sizeof(float);
     s->image_bytes = (size_t)c->image_width * c->image_height * 3 * sizeof(float);
+    if (is_tiled(c)) {
+        s->region_x = std::max(0, c->tile_x - c->tile_halo);
+        s->region_y = std::max(0, c->tile_y - c->tile_halo);
+        s->region_width = std::min(c->image_width, c->tile_x + c->tile_width + c->tile_halo) - s->region_x;
+        s->region_height = std::min(c->image_height, c->tile_y + c->tile_height + c->tile_halo) - s->region_y;
+    } else {
+        s->region_x = s->region_y = 0;
+        s->region_width = c->image_width;
+        s->region_height = c->image_height;
+    }
+    s->region_bytes = (size_t)s->region_width * s->region_height * 3 * sizeof(float);
     return BMFR_OK;
 }
 
@@ -201,7 +268,7 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
     c->sizes = sz;
     c->P = make_params(cfg, &sz);
     c->device = device;
-    const size_t px = (size_t)cfg->image_width * cfg->image_height;
+    const size_t px = (size_t)sz.region_width * sz.region_height;  // every plane covers the region
     hipError_t e = hipSuccess;
     for (int i = 0; i < 2 && e == hipSuccess; ++i) {
         e = hipMalloc(&c->noisy_acc[i], px * 3 * sizeof(float));
@@ -213,7 +280,7 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
     if (e == hipSuccess) e = hipMalloc(&c->prev_pixel, px * sizeof(float2));
     if (e == hipSuccess && std::getenv("BMFR_STAMPS"))
         e = hipMalloc(&c->stamps, (size_t)sz.blocks * 8 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&c->noise_table, (size_t)bmfr::kMaxFeatures * bmfr::kBlockPixels * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&c->noise_table, (size_t)bmfr::kMaxFeatures * bmfr::kBlockPixels * sizeof(double));
     if (e != hipSuccess) {
         bmfr_destroy(c);
         return hip_status(e);
@@ -261,6 +328,7 @@ bmfr_status bmfr_accumulate_noisy_data(bmfr_ctx* c, void* stream, float* out_pre
         !current_noisy || !current_spp || !tmp_data || !prev_frame_camera_matrix || !pixel_offset ||
         frame_number < 0)
         return BMFR_ERROR_INVALID_ARGUMENT;
+    if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // stage kernels use the whole-frame layout
     if (frame_number > 0 && (!previous_normals || !previous_positions || !previous_noisy || !previous_spp))
         return BMFR_ERROR_INVALID_ARGUMENT;
     bmfr::NoisyInputs in{current_normals, previous_normals, current_positions, previous_positions,
@@ -274,6 +342,7 @@ bmfr_status bmfr_accumulate_noisy_data(bmfr_ctx* c, void* stream, float* out_pre
 bmfr_status bmfr_fitter(bmfr_ctx* c, void* stream, float* weights, float* mins_maxs, void* tmp_data,
                         int frame_number) {
     if (!c || !weights || !mins_maxs || !tmp_data || frame_number < 0) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // stage kernels use the whole-frame layout
     if (!bmfr::fitter_supported(c->P.not_scaled, c->P.scaled)) return BMFR_ERROR_UNSUPPORTED;
     return hip_status(bmfr::launch_fitter(c->P, as_stream(stream), weights, mins_maxs, tmp_data, frame_number));
 }
@@ -285,6 +354,7 @@ bmfr_status bmfr_weighted_sum(bmfr_ctx* c, void* stream, const float* weights, c
     (void)current_noisy;  // debugging-only argument upstream (bmfr.cl:709)
     if (!c || !weights || !mins_maxs || !output || !current_normals || !current_positions || frame_number < 0)
         return BMFR_ERROR_INVALID_ARGUMENT;
+    if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // stage kernels use the whole-frame layout
     return hip_status(bmfr::launch_weighted_sum(c->P, as_stream(stream), weights, mins_maxs, output,
                                                 current_normals, current_positions, frame_number));
 }
@@ -297,6 +367,7 @@ bmfr_status bmfr_accumulate_filtered_data(bmfr_ctx* c, void* stream, const float
     if (!c || !filtered_frame || !in_prev_frame_pixel || !accept_bools || !albedo || !tone_mapped_frame ||
         !current_spp || !accumulated_frame || frame_number < 0)
         return BMFR_ERROR_INVALID_ARGUMENT;
+    if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // stage kernels use the whole-frame layout
     if (frame_number > 0 && !accumulated_prev_frame) return BMFR_ERROR_INVALID_ARGUMENT;
     return hip_status(bmfr::launch_accumulate_filtered(
         c->P, as_stream(stream), filtered_frame, reinterpret_cast<const float2*>(in_prev_frame_pixel),
@@ -308,6 +379,7 @@ bmfr_status bmfr_taa(bmfr_ctx* c, void* stream, const float* in_prev_frame_pixel
                      float* result_frame, const float* prev_frame, int frame_number) {
     if (!c || !in_prev_frame_pixel || !new_frame || !result_frame || frame_number < 0)
         return BMFR_ERROR_INVALID_ARGUMENT;
+    if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // stage kernels use the whole-frame layout
     if (frame_number > 0 && !prev_frame) return BMFR_ERROR_INVALID_ARGUMENT;
     return hip_status(bmfr::launch_taa(c->P, as_stream(stream),
                                        reinterpret_cast<const float2*>(in_prev_frame_pixel), new_frame,
@@ -324,6 +396,7 @@ bmfr_status bmfr_process_frame(bmfr_ctx* c, void* stream, const bmfr_frame_input
     if (frame_number > 0 && (!in->prev_normals || !in->prev_positions || !c->has_frame))
         return BMFR_ERROR_INVALID_ARGUMENT;
     if (!bmfr::fitter_supported(c->P.not_scaled, c->P.scaled)) return BMFR_ERROR_UNSUPPORTED;
+    if (is_tiled(&c->cfg) && !bmfr::fused_supported(c->P)) return BMFR_ERROR_UNSUPPORTED;
     const int cur = c->has_frame ? 1 - c->cur : 0;  // swap, bmfr.cpp:482-484
     const int prv = 1 - cur;
     hipEvent_t* ev = nullptr;
@@ -349,7 +422,8 @@ bmfr_status bmfr_process_frame(bmfr_ctx* c, void* stream, const bmfr_frame_input
     A.result_out = c->result[cur];
     A.noise_table = c->noise_table;
     A.stamps = c->stamps;
-    const bmfr_status st = hip_status(bmfr::launch_fused_frame(c->P, as_stream(stream), A, ev ? ev[1] : nullptr));
+    const bmfr_status st =
+        hip_status(bmfr::launch_fused_frame(frame_params(c, frame_number), as_stream(stream), A, ev ? ev[1] : nullptr));
     if (st != BMFR_OK) return st;
     if (ev) {
         (void)hipEventRecord(ev[2], as_stream(stream));

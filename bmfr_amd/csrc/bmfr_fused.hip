@@ -148,7 +148,7 @@ __device__ __forceinline__ void block_reduce(float (&v)[K], K1Lds<B>& L, int t) 
 // One Householder column (bmfr.cl:549-655), compile-time column index.
 // ---------------------------------------------------------------------------
 template <int col, int B, class M>
-__device__ __forceinline__ void qr_column(M& A, K1Lds<B>& L, int t, const float* __restrict__ noise,
+__device__ __forceinline__ void qr_column(M& A, K1Lds<B>& L, int t, const double* __restrict__ noise,
                                           double noise2) {
     constexpr int RE = B - 2;
     constexpr int cl = col;  // col_limited (feature columns only)
@@ -179,7 +179,7 @@ __device__ __forceinline__ void qr_column(M& A, K1Lds<B>& L, int t, const float*
                     for (int s = 0; s < kSubs; ++s) {
                         float v = A.get(fb, s);
                         if (fb < B - 3)
-                            v = (float)((double)v + noise2 * (double)noise[(fb - 1) * kBlockPixels + t + kLocal * s]);
+                            v = (float)((double)v + noise[(fb - 1) * kBlockPixels + t + kLocal * s]);
                         vals[k][s] = v;
                     }
                     float sum = row0 ? vals[k][0] * -31.f : vals[k][0];
@@ -261,7 +261,7 @@ __device__ __forceinline__ void qr_column(M& A, K1Lds<B>& L, int t, const float*
 }
 
 template <int B, class M, int... C>
-__device__ __forceinline__ void qr_columns(M& A, K1Lds<B>& L, int t, const float* __restrict__ noise,
+__device__ __forceinline__ void qr_columns(M& A, K1Lds<B>& L, int t, const double* __restrict__ noise,
                                            double noise2, std::integer_sequence<int, C...>) {
     (qr_column<C, B>(A, L, t, noise, noise2), ...);
 }
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
                                                     uint8_t* __restrict__ spp_out,
                                                     float2* __restrict__ prev_pixel_out,
                                                     float* __restrict__ acc_out,
-                                                    const float* __restrict__ noise,
+                                                    const double* __restrict__ noise,
                                                     unsigned long long* __restrict__ stamps) {
     constexpr int B = NS + FS + 3;
     __shared__ K1Lds<B> L;
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
 #define BMFR_STAMP(k) (void)stamps
 #endif
     BMFR_STAMP(0);
-    const int bx = g % P.blocks_x, by = g / P.blocks_x;
+    const int bx = P.bx0 + g % P.nbx, by = P.by0 + g / P.nbx;
 
     // ---- accumulate_noisy_data (bmfr.cl:310-484) for rows t + 256s ----
     Rows<B, HALF> A;
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
         const int px = bx * kEdge + (t3 & (kEdge - 1)) - kEdge / 2 + off.x;
         const int py = by * kEdge + (t3 >> 5) + 8 * s - kEdge / 2 + off.y;
         // non-owned rows (margins) read a valid pixel and are then skipped
-        lin[s] = (bits[s] & 1u) ? (long)py * P.width + px : 0;
+        lin[s] = pix(P, (bits[s] & 1u) ? px : P.ox, (bits[s] & 1u) ? py : P.oy);
         n[s] = ld3(in.n_cur, lin[s]);
         pos[s] = ld3(in.p_cur, lin[s]);
         pp[s] = prev_pixel_out[lin[s]];
@@ -472,11 +472,11 @@ bool fused_supported(const Params& P) {
 template <int NS, int FS, bool HALF>
 static void launch_k1(const Params& P, hipStream_t st, const FusedArgs& A) {
     if (k1_tone_maps(P))
-        hipLaunchKernelGGL((k_fused<NS, FS, HALF, true>), dim3(P.blocks_x * P.blocks_y), dim3(kThreads), 0, st, P,
+        hipLaunchKernelGGL((k_fused<NS, FS, HALF, true>), dim3(P.nbx * P.nby), dim3(kThreads), 0, st, P,
                            A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
                            A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
     else
-    hipLaunchKernelGGL((k_fused<NS, FS, HALF, false>), dim3(P.blocks_x * P.blocks_y), dim3(kThreads), 0, st, P, A.in,
+    hipLaunchKernelGGL((k_fused<NS, FS, HALF, false>), dim3(P.nbx * P.nby), dim3(kThreads), 0, st, P, A.in,
                        A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out, A.acc_out,
                        A.noise_table, A.stamps);
 }

@@ -38,20 +38,32 @@ constexpr int kUStride = 20;  // floats per lane in a u buffer: 16 + 4 (conflict
 
 template <int B>
 struct Lds {
+#ifdef BMFR_KEEP_ALIAS
+    // phase 1 -> 3: previous accumulated filtered colour per item, held in
+    // registers through phase 1 and parked in the matrix area once it is free
+    static constexpr bool kKeepAlias = true;
     union {
         _Float16 M[B - 1][64 * kSlots];  // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
         struct {
-            float u[2][64 * kUStride];  // Householder vectors, double-buffered by column parity
-            float keep[4][3][kThreads];  // phase 1 -> 3: previous accumulated filtered colour per item
+            float u[2][64 * kUStride];    // Householder vectors, double-buffered by column parity
+            float keep[4][3][kThreads];
         };
     };
+#else
+    static constexpr bool kKeepAlias = false;
+    union {
+        _Float16 M[B - 1][64 * kSlots];  // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
+        float u[2][64 * kUStride];       // Householder vectors, double-buffered by column parity
+    };
+    float keep[4][3][kThreads];  // phase 1 -> 3: previous accumulated filtered colour per item
+#endif
     float piv[2][2];                    // |u|^2 and RN(1/|u|^2) of the published vector
     float R[(B - 2) * (B - 2) * 3];     // R[x][y][ch], x = column (as k_fused)
     float weights[(B - 3) * 3];
     float mm[3 * (B - 3)];              // per scaled feature: min, max, 1/(max-min)
 };
 static_assert(sizeof(float) * (2 * 64 * kUStride + 4 * 3 * kThreads) <= sizeof(_Float16) * 12 * 64 * kSlots,
-              "u buffers + phase-3 colours must fit in the matrix area (B >= 13)");
+              "u buffers and parked colours must fit in the matrix area (B >= 13)");
 
 template <int... I, class F>
 __device__ __forceinline__ void sfor_impl(std::integer_sequence<int, I...>, F&& f) {
@@ -75,6 +87,28 @@ __device__ __forceinline__ float wave_reduce(const float (&p)[4]) {
     return wave_tree<OP>(step2<OP>(p));
 }
 
+// Mixed-precision FMAs on one half of a packed pair (f16 -> f32 is exact, one
+// rounding): RN(h * b) (fma with -0 addend: exact product, sign of zero kept)
+// and RN(h - q), without separate conversions.
+template <int HI>
+__device__ __forceinline__ float mul_h(h2 h, float b) {
+    float r;
+    if constexpr (HI)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(b), "s"(-0.0f));
+    else
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(b), "s"(-0.0f));
+    return r;
+}
+template <int HI>
+__device__ __forceinline__ float sub_h(h2 h, float q) {
+    float r;
+    if constexpr (HI)
+        asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(q));
+    else
+        asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(q));
+    return r;
+}
+
 // Column update of Householder step c >= 1 (bmfr.cl:603-653) on one column:
 // dot with u over rows >= c, then A -= (2u) dot / |u|^2 on those rows.
 // With the fast path, the division is a Markstein step on the shared
@@ -83,9 +117,6 @@ __device__ __forceinline__ float wave_reduce(const float (&p)[4]) {
 template <int c>
 __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
                                               int l) {
-    float x[kSlots];
-#pragma unroll
-    for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
     float p[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -93,29 +124,32 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
 #pragma unroll
         for (int si = 0; si < 4; ++si) {
             const int j = m + 4 * si;
-            float pr = x[j] * u[j];
+            float pr = (j & 1) ? mul_h<1>(a[j >> 1], u[j]) : mul_h<0>(a[j >> 1], u[j]);
             if (j == 0) pr = l >= c ? pr : 0.f;  // rows above the pivot: skipped (0.f + 0.f + ... is the same sum)
             s = s + pr;
         }
         p[m] = s;
     }
     const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);  // (2u) dot == u (2 dot): same real product, one rounding
-    float nv[kSlots];
+    float q[kSlots];
     if (fabsf(c2) < 0x1p100f && ulen2 >= 0x1p-100f && ulen2 < 0x1p100f) {
 #pragma unroll
-        for (int j = 0; j < kSlots; ++j) nv[j] = x[j] - div_by_recip(u[j] * c2, ulen2, recip);
+        for (int j = 0; j < kSlots; ++j) q[j] = div_by_recip(u[j] * c2, ulen2, recip);
     } else {
         float c2s = c2;  // opaque: keeps the products inside this (cold) branch
         asm volatile("" : "+v"(c2s));
 #pragma unroll
         for (int j = 0; j < kSlots; ++j) {
-            nv[j] = x[j] - (u[j] * c2s) / ulen2;
+            q[j] = (u[j] * c2s) / ulen2;
             __builtin_amdgcn_sched_barrier(0);  // never taken in practice: keep it narrow
         }
     }
-    nv[0] = l >= c ? nv[0] : x[0];
+    q[0] = l >= c ? q[0] : 0.f;  // x - (+0) == x: rows above the pivot keep their value
 #pragma unroll
-    for (int j = 0; j < kSlots; ++j) a[j >> 1][j & 1] = (_Float16)nv[j];
+    for (int k = 0; k < kSlots / 2; ++k) {
+        const float n0 = sub_h<0>(a[k], q[2 * k]), n1 = sub_h<1>(a[k], q[2 * k + 1]);
+        a[k] = h2{(_Float16)n0, (_Float16)n1};
+    }
     __builtin_amdgcn_sched_barrier(0);  // one column in flight: bounds the register footprint
 }
 
@@ -123,12 +157,15 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
 // |u|^2 = 1984 and u*x = x exactly (see k_fused's qr_column<0>).  Noise is
 // added to feature columns on this first load (bmfr.cl:625-627).
 template <bool NOISE>
-__device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const float* __restrict__ noise, double noise2) {
+__device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const double* __restrict__ noise, double noise2) {
     float x[kSlots];
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) {
         x[j] = hget(a, j);
-        if (NOISE) x[j] = (float)((double)x[j] + noise2 * (double)noise[l + 64 * j]);
+        if (NOISE) {
+            x[j] = (float)((double)x[j] + noise[l + 64 * j]);
+            if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // 8 double loads in flight at a time
+        }
     }
     float p[4];
 #pragma unroll
@@ -215,7 +252,7 @@ struct WaveFit {
     static constexpr bool owns(int c) { return c >= 1 && c < B && (c & 3) == W; }
 
     template <int c>
-    static __device__ __forceinline__ void step(h2 (&a)[NSL][8], Lds<B>& L, int l, const float* __restrict__ noise,
+    static __device__ __forceinline__ void step(h2 (&a)[NSL][8], Lds<B>& L, int l, const double* __restrict__ noise,
                                                 double noise2) {
         constexpr int nxt = c + 1;
         constexpr bool publish = nxt < NF && owns(nxt);
@@ -262,14 +299,14 @@ struct WaveFit {
     }
 
     template <int... C>
-    static __device__ __forceinline__ void steps(h2 (&a)[NSL][8], Lds<B>& L, int l, const float* __restrict__ noise,
+    static __device__ __forceinline__ void steps(h2 (&a)[NSL][8], Lds<B>& L, int l, const double* __restrict__ noise,
                                                  double noise2, std::integer_sequence<int, C...>) {
         (step<C>(a, L, l, noise, noise2), ...);
     }
 
     // after_load(): runs once the matrix is in registers and the LDS area is free.
     template <class AfterLoad>
-    static __device__ __forceinline__ void run(Lds<B>& L, int l, const float* __restrict__ noise, double noise2,
+    static __device__ __forceinline__ void run(Lds<B>& L, int l, const double* __restrict__ noise, double noise2,
                                                AfterLoad&& after_load) {
         h2 a[NSL][8];
         sfor<NSL>([&](auto K) {
@@ -370,7 +407,7 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
                                                           uint8_t* __restrict__ spp_out,
                                                           float2* __restrict__ prev_pixel_out,
                                                           float* __restrict__ acc_out,
-                                                          const float* __restrict__ noise,
+                                                          const double* __restrict__ noise,
                                                           unsigned long long* __restrict__ stamps) {
     constexpr int B = NS + FS + 3;
     __shared__ Lds<B> L;
@@ -385,7 +422,7 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 #define BMFR_STAMP(k) (void)stamps
 #endif
     BMFR_STAMP(0);
-    const int bx = g % P.blocks_x, by = g / P.blocks_x;
+    const int bx = P.bx0 + g % P.nbx, by = P.by0 + g / P.nbx;
     const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
 
     // ---- accumulate_noisy_data (bmfr.cl:310-484), rows l + 64 (4w + i) ----
@@ -416,22 +453,34 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
                 else v = f == B - 3 ? it.color.x : (f == B - 2 ? it.color.y : it.color.z);
                 if (__builtin_isnan(v)) v = 0.0f;              // bmfr.cl:468-469
                 v = fmaxf(fminf(v, 65504.f), -65504.f);         // bmfr.cl:471-473
+#ifdef BMFR_P1_B16
+                L.M[f - 1][l * kSlots + 4 * w + i] = (_Float16)v;
+#else
                 pk[f][i & 1] = (_Float16)v;
+#endif
             }
             spps |= (uint32_t)it.spp << (8 * i);
             ibits |= ((uint32_t)it.owner << i) | ((uint32_t)it.prev_f_divided << (4 + i));
-            keep_prev[i] = it.prev_f;
+            if constexpr (Lds<B>::kKeepAlias) {
+                keep_prev[i] = it.prev_f;
+            } else {
+                L.keep[i][0][t] = it.prev_f.x;  // parked for phase 3
+                L.keep[i][1][t] = it.prev_f.y;
+                L.keep[i][2][t] = it.prev_f.z;
+            }
             if (it.owner) {
                 st3(noisy_out, it.lin, it.color);
                 spp_out[it.lin] = it.spp;
                 prev_pixel_out[it.lin] = make_float2(it.pfx, it.pfy);
             }
+#ifndef BMFR_P1_B16
             if (i & 1) {  // rows j = 4w + i - 1, 4w + i: adjacent halves of lane l's row slot
 #pragma unroll
                 for (int f = 1; f < B; ++f)
                     *reinterpret_cast<uint32_t*>(&L.M[f - 1][l * kSlots + 4 * w + i - 1]) =
                         __builtin_bit_cast(uint32_t, pk[f]);
             }
+#endif
 #ifdef BMFR_P1_SERIAL
             __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -443,11 +492,13 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 
     // ---- fit: min/max scaling, Householder QR, right-hand side ----
     const auto park = [&] {
+        if constexpr (Lds<B>::kKeepAlias) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            L.keep[i][0][t] = keep_prev[i].x;
-            L.keep[i][1][t] = keep_prev[i].y;
-            L.keep[i][2][t] = keep_prev[i].z;
+            for (int i = 0; i < 4; ++i) {
+                L.keep[i][0][t] = keep_prev[i].x;
+                L.keep[i][1][t] = keep_prev[i].y;
+                L.keep[i][2][t] = keep_prev[i].z;
+            }
         }
     };
     switch (w) {
@@ -472,7 +523,7 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
     for (int i = 0; i < 4; ++i) {
         const int px = bx * kEdge + (l3 & (kEdge - 1)) - kEdge / 2 + off.x;
         const int py = by * kEdge + (l3 >> 5) + 8 * w + 2 * i - kEdge / 2 + off.y;
-        lin[i] = (ibits & (1u << i)) ? (long)py * P.width + px : 0;  // margins: a valid pixel, skipped below
+        lin[i] = pix(P, (ibits & (1u << i)) ? px : P.ox, (ibits & (1u << i)) ? py : P.oy);  // margins: a valid pixel, skipped below
         nrm[i] = ld3(in.n_cur, lin[i]);
         wp[i] = ld3(in.p_cur, lin[i]);
     }
@@ -521,7 +572,7 @@ bool fused_cols_supported(const Params& P) {
 }
 
 hipError_t launch_fused_k1_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
-    const dim3 grid(P.blocks_x * P.blocks_y), block(cols::kThreads);
+    const dim3 grid(P.nbx * P.nby), block(cols::kThreads);
     if (P.scaled == 6)
         hipLaunchKernelGGL((cols::k_fused_cols<4, 6>), grid, block, 0, st, P, A.in, A.cam, A.frame, A.acc_prev,
                            A.noisy_out, A.spp_out, A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);

@@ -107,6 +107,14 @@ struct Camera {
     float jx, jy;  // this frame's pixel offset
 };
 
+// Linear index of image pixel (x, y) in a plane of the buffer region, and
+// clamps into the region (= the image when untiled).
+__device__ __forceinline__ long pix(const Params& P, int x, int y) {
+    return (long)(y - P.oy) * P.stride + (x - P.ox);
+}
+__device__ __forceinline__ int clamp_rx(const Params& P, int x) { return min(max(x, P.ox), P.ox + P.stride - 1); }
+__device__ __forceinline__ int clamp_ry(const Params& P, int y) { return min(max(y, P.oy), P.oy + P.rows - 1); }
+
 __device__ __forceinline__ NoisyItem noisy_item(const Params& P, const NoisyInputs& in,
                                                 const Camera& cam, int gx, int gy, int frame) {
     NoisyItem o;
@@ -210,7 +218,7 @@ __device__ __forceinline__ NoisyCur noisy_load_current(const Params& P, const No
     c.px = mirror(ux, P.width);
     c.py = mirror(uy, P.height);
     c.owner = ux >= 0 && ux < P.width && uy >= 0 && uy < P.height;
-    const long lin = (long)c.py * P.width + c.px;
+    const long lin = pix(P, c.px, c.py);
     c.wp = ld3(in.p_cur, lin);
     c.nrm = ld3(in.n_cur, lin);
     c.cur = ld3(in.noisy_cur, lin);
@@ -223,7 +231,7 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
                                                      const float* __restrict__ acc_prev = nullptr) {
     NoisyItem o;
     o.owner = c.owner;
-    o.lin = (long)c.py * P.width + c.px;
+    o.lin = pix(P, c.px, c.py);
     o.n = c.nrm;
     o.p = c.wp;
     const f3 wp = c.wp, nrm = c.nrm, cur = c.cur;
@@ -264,7 +272,7 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
         for (int i = 0; i < 4; ++i) {
             const int sx = ix + (i & 1), sy = iy + (i >> 1);
             inb[i] = sx >= 0 && sy >= 0 && sx < P.width && sy < P.height;
-            const long s = (long)min(max(sy, 0), P.height - 1) * P.width + min(max(sx, 0), P.width - 1);
+            const long s = pix(P, clamp_rx(P, sx), clamp_ry(P, sy));
             pp[i] = ld3(in.p_prev, s);
             pn[i] = ld3(in.n_prev, s);
             pc[i] = ld3(in.noisy_prev, s);
@@ -542,7 +550,7 @@ __device__ __forceinline__ f3 blend_filtered(const Params& P, f3 filtered, float
         for (int i = 0; i < 4; ++i) {
             if (acc_bits & (1 << i)) {
                 total = total + wts[i];
-                const f3 pc = ld3(acc_prev, (long)(iy + (i >> 1)) * P.width + ix + (i & 1));
+                const f3 pc = ld3(acc_prev, pix(P, ix + (i & 1), iy + (i >> 1)));
                 prev.x = prev.x + wts[i] * pc.x;
                 prev.y = prev.y + wts[i] * pc.y;
                 prev.z = prev.z + wts[i] * pc.z;
@@ -607,8 +615,7 @@ __device__ __forceinline__ f3 taa_pixel(const Params& P, int x, int y, f3 me, f3
     f3 pc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // taps loaded up front (clamped address when skipped)
-        const int sx = min(max(ix + (i & 1), 0), W - 1), sy = min(max(iy + (i >> 1), 0), H - 1);
-        pc[i] = ld3(prev_frame, (long)sy * W + sx);
+        pc[i] = ld3(prev_frame, pix(P, clamp_rx(P, ix + (i & 1)), clamp_ry(P, iy + (i >> 1))));
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // bmfr.cl:929-960

@@ -166,13 +166,15 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
     __shared__ float T[3][N];  // RGB
     __shared__ float Y[3][N];  // YCoCg
     const int t = threadIdx.x;
-    const int x0 = blockIdx.x * kTaaW, y0 = blockIdx.y * kTaaH;
+    // Output tile of this launch (the whole image, or a multi-GPU tile whose
+    // one-pixel halo lies inside the buffer region).
+    const int x0 = P.tx0 + blockIdx.x * kTaaW, y0 = P.ty0 + blockIdx.y * kTaaH;
     f3 v[ITER], al[ITER];
 #pragma unroll
     for (int k = 0; k < ITER; ++k) {  // all tile loads in flight first
         const int i = t + 256 * k;
         const int x = min(max(x0 - 1 + i % HW, 0), P.width - 1), y = min(max(y0 - 1 + i / HW, 0), P.height - 1);
-        const long lin = (long)y * P.width + x;
+        const long lin = pix(P, x, y);
         v[k] = ld3(src, lin);
         if (TONE) al[k] = ld3(albedo, lin);
     }
@@ -195,14 +197,14 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
     float2 pf[kTaaH / 4];
 #pragma unroll
     for (int k = 0; k < kTaaH / 4; ++k) {
-        const int x = min(x0 + tx, P.width - 1), y = min(y0 + (t >> 6) + 4 * k, P.height - 1);
-        pf[k] = prev_pixel[(long)y * P.width + x];
+        const int x = min(x0 + tx, P.tx1 - 1), y = min(y0 + (t >> 6) + 4 * k, P.ty1 - 1);
+        pf[k] = prev_pixel[pix(P, x, y)];
     }
 #pragma unroll
     for (int k = 0; k < kTaaH / 4; ++k) {
         const int ty = (t >> 6) + 4 * k;
         const int x = x0 + tx, y = y0 + ty;
-        if (x < P.width && y < P.height) {
+        if (x < P.tx1 && y < P.ty1) {
             const int c = (ty + 1) * HW + tx + 1;
             const f3 me{T[0][c], T[1][c], T[2][c]};
             const f3 me_y{Y[0][c], Y[1][c], Y[2][c]};
@@ -210,7 +212,7 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
                 const int n = c + dy * HW + dx;
                 return f3{Y[0][n], Y[1][n], Y[2][n]};
             });
-            st3(result, (long)y * P.width + x, r);
+            st3(result, pix(P, x, y), r);
         }
     }
 }
@@ -282,11 +284,14 @@ __global__ __launch_bounds__(256) void k_fused_block(Params P, NoisyInputs in, C
 // feature and the frame, never on the block; K1 reads it from this table
 // instead of re-hashing per element: table[(fb-1)*1024 + row] = random() - 0.5f
 // for fb = 1..B-4; the kernel forms NOISE_AMOUNT*2.f*that in double as upstream.
-__global__ __launch_bounds__(256) void k_noise_table(int frame, int buffers, float* __restrict__ table) {
+__global__ __launch_bounds__(256) void k_noise_table(int frame, int buffers, double noise2,
+                                                     double* __restrict__ table) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (buffers - 4) * kBlockPixels) return;
     const int fb = 1 + i / kBlockPixels, r = i % kBlockPixels;
-    table[i] = hash_random((uint32_t)(r + fb * kBlockPixels + frame * buffers * kBlockPixels)) - 0.5f;
+    // add_random's addend (bmfr.cl:173-182) for row r of feature fb: the same
+    // for every block, so computed once per frame.
+    table[i] = noise2 * (double)(hash_random((uint32_t)(r + fb * kBlockPixels + frame * buffers * kBlockPixels)) - 0.5f);
 }
 
 // ---------------------------------------------------------------- launch --
@@ -369,12 +374,12 @@ hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& 
     hipError_t e;
     if (fused_supported(P)) {
         const int n = (P.buffers - 4) * kBlockPixels;
-        hipLaunchKernelGGL(k_noise_table, dim3((n + 255) / 256), dim3(256), 0, st, A.frame, P.buffers,
+        hipLaunchKernelGGL(k_noise_table, dim3((n + 255) / 256), dim3(256), 0, st, A.frame, P.buffers, P.noise2,
                            A.noise_table);
         e = fused_cols_supported(P) ? launch_fused_k1_cols(P, st, A) : launch_fused_k1(P, st, A);
         if (e != hipSuccess) return e;
         if (mid) (void)hipEventRecord(mid, st);
-        const dim3 grd((P.width + kTaaW - 1) / kTaaW, (P.height + kTaaH - 1) / kTaaH);
+        const dim3 grd((P.tx1 - P.tx0 + kTaaW - 1) / kTaaW, (P.ty1 - P.ty0 + kTaaH - 1) / kTaaH);
         if (k1_tone_maps(P))
             hipLaunchKernelGGL(k_fused_taa<false>, grd, dim3(256), 0, st, P, A.tone_out, A.albedo,
                                A.prev_pixel_out, A.result_out, A.result_prev, A.frame);

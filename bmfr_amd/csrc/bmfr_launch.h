@@ -21,7 +21,7 @@ struct FusedArgs {
     float* acc_out;
     float* tone_out;
     float* result_out;
-    float* noise_table;  // (B-4) * 1024 floats, context-owned
+    double* noise_table;  // (B-4) * 1024 noise terms NOISE_AMOUNT*2*(rnd-0.5) in double, context-owned
     unsigned long long* stamps;  // diagnostic build: 8 timestamps per block, or null
 };
 

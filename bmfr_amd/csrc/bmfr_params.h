@@ -36,6 +36,20 @@ struct Params {
     float position_limit_sq, normal_limit_sq;
     int half_tmp;                 // USE_HALF_PRECISION_IN_TMP_DATA
     int fused_variant;            // 0 = default, 1 = generic-feature K1, 2 = tone map in K1, 3 = row-split K1 (A/B diagnostics)
+    // Buffer region (multi-GPU tiles): every plane of the fused path holds the
+    // image pixels [ox, ox + stride) x [oy, oy + rows), row stride `stride`.
+    // Untiled: 0, 0, width, height -- the reference's layout.
+    int ox, oy, stride, rows;
+    // Per launch: the blocks of the shifted grid K1 covers (bx0 + g % nbx,
+    // by0 + g / nbx) and the output tile [tx0, tx1) x [ty0, ty1) of K2.
+    int bx0, by0, nbx, nby;
+    int tx0, ty0, tx1, ty1;
 };
+
+// BLOCK_OFFSETS (bmfr.cl:267-285), host copy of the device table in
+// bmfr_device.h: the grid shift of frame f is kBlockOffsetTable[f % 16].
+constexpr int kBlockOffsetTable[16][2] = {
+    {-14, -14}, {4, -6}, {-8, 14}, {8, 0}, {-10, -8}, {2, 12}, {12, -12}, {-10, 0},
+    {12, 14}, {-8, -16}, {6, 6}, {-2, -2}, {6, -14}, {-16, 12}, {14, -4}, {-6, 4}};
 
 }  // namespace bmfr

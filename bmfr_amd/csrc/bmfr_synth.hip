@@ -75,10 +75,13 @@ HD inline uint32_t mix32(uint32_t h) {
 // Camera of frame f in double precision (host), like a renderer would export it.
 void camera_frame(int W, int H, int f, double eye[3], double right[3], double up[3], double fwd[3],
                   double* tan_x, double* tan_y) {
-    const double yaw = 0.35 - 0.0012 * f, pitch = -0.12 + 0.0004 * f;
-    eye[0] = -2.0 + 0.012 * f;
-    eye[1] = 2.0 + 0.002 * f;
-    eye[2] = 9.0 - 0.025 * f;
+    // Slow pan + dolly: about 1.1 px/frame at 960 px wide (4.5 at 3840),
+    // proportional to the resolution like a real camera (SURVEY.md 8d asks
+    // for a slow pan; the tiled path's halo must cover this motion).
+    const double yaw = 0.35 - 0.0003 * f, pitch = -0.12 + 0.0001 * f;
+    eye[0] = -2.0 + 0.003 * f;
+    eye[1] = 2.0 + 0.0005 * f;
+    eye[2] = 9.0 - 0.00625 * f;
     fwd[0] = -std::sin(yaw) * std::cos(pitch);
     fwd[1] = std::sin(pitch);
     fwd[2] = -std::cos(yaw) * std::cos(pitch);
@@ -172,7 +175,8 @@ HD inline V3 irradiance(V3 p, V3 n) {
     return e;
 }
 
-HD inline void shade_pixel(int W, int H, int x, int y, int frame, uint32_t seed, const CameraBasis& b,
+// Pixel (x, y) of the W x H frame, stored at element 3*o of the planes.
+HD inline void shade_pixel(int W, int H, int x, int y, long o, int frame, uint32_t seed, const CameraBasis& b,
                            float* noisy, float* normals, float* positions, float* albedo, float* clean) {
     const float nx = 2.f * ((float)x + b.jx) / (float)W - 1.f;
     const float ny = 2.f * ((float)y + 1.f - b.jy) / (float)H - 1.f;
@@ -180,7 +184,7 @@ HD inline void shade_pixel(int W, int H, int x, int y, int frame, uint32_t seed,
     d = mul(d, 1.f / sqrtf(dotv(d, d)));
     const Hit h = trace(b.eye, d);
     const V3 e = irradiance(h.p, h.n);
-    const long i = 3L * ((long)y * W + x);
+    const long i = 3L * o;
     float ec[3] = {e.x, e.y, e.z};
     const uint32_t base = mix32(seed ^ mix32((uint32_t)frame * 0x9E3779B1u + 0x632BE5ABu)) ^
                           (uint32_t)((long)y * W + x) * 0x85EBCA77u;
@@ -209,12 +213,14 @@ HD inline void shade_pixel(int W, int H, int x, int y, int frame, uint32_t seed,
     }
 }
 
-__global__ void k_synth(int W, int H, int frame, uint32_t seed, CameraBasis b, float* noisy, float* normals,
-                        float* positions, float* albedo, float* clean) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y * blockDim.y + threadIdx.y;
-    if (x >= W || y >= H) return;
-    shade_pixel(W, H, x, y, frame, seed, b, noisy, normals, positions, albedo, clean);
+// The region [x0, x0 + rw) x [y0, y0 + rh) of the frame, planes of row stride rw.
+__global__ void k_synth(int W, int H, int x0, int y0, int rw, int rh, int frame, uint32_t seed, CameraBasis b,
+                        float* noisy, float* normals, float* positions, float* albedo, float* clean) {
+    const int rx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ry = blockIdx.y * blockDim.y + threadIdx.y;
+    if (rx >= rw || ry >= rh) return;
+    shade_pixel(W, H, x0 + rx, y0 + ry, (long)ry * rw + rx, frame, seed, b, noisy, normals, positions, albedo,
+                clean);
 }
 
 }  // namespace
@@ -251,19 +257,28 @@ bmfr_status bmfr_synth_frame_host(int W, int H, int frame, uint32_t seed, float*
         return BMFR_ERROR_INVALID_ARGUMENT;
     const CameraBasis b = basis(W, H, frame);
     for (int y = 0; y < H; ++y)
-        for (int x = 0; x < W; ++x) shade_pixel(W, H, x, y, frame, seed, b, noisy, normals, positions, albedo, clean);
+        for (int x = 0; x < W; ++x)
+            shade_pixel(W, H, x, y, (long)y * W + x, frame, seed, b, noisy, normals, positions, albedo, clean);
     return BMFR_OK;
+}
+
+bmfr_status bmfr_synth_region_device(int W, int H, int x0, int y0, int rw, int rh, int frame, uint32_t seed,
+                                     float* noisy, float* normals, float* positions, float* albedo, float* clean,
+                                     void* stream) {
+    if (W <= 0 || H <= 0 || frame < 0 || !noisy || !normals || !positions || !albedo || x0 < 0 || y0 < 0 ||
+        rw <= 0 || rh <= 0 || x0 + rw > W || y0 + rh > H)
+        return BMFR_ERROR_INVALID_ARGUMENT;
+    const CameraBasis b = basis(W, H, frame);
+    const dim3 blk(64, 4), grd((rw + 63) / 64, (rh + 3) / 4);
+    hipLaunchKernelGGL(k_synth, grd, blk, 0, reinterpret_cast<hipStream_t>(stream), W, H, x0, y0, rw, rh, frame,
+                       seed, b, noisy, normals, positions, albedo, clean);
+    return hipGetLastError() == hipSuccess ? BMFR_OK : BMFR_ERROR_HIP;
 }
 
 bmfr_status bmfr_synth_frame_device(int W, int H, int frame, uint32_t seed, float* noisy, float* normals,
                                     float* positions, float* albedo, float* clean, void* stream) {
-    if (W <= 0 || H <= 0 || frame < 0 || !noisy || !normals || !positions || !albedo)
-        return BMFR_ERROR_INVALID_ARGUMENT;
-    const CameraBasis b = basis(W, H, frame);
-    const dim3 blk(64, 4), grd((W + 63) / 64, (H + 3) / 4);
-    hipLaunchKernelGGL(k_synth, grd, blk, 0, reinterpret_cast<hipStream_t>(stream), W, H, frame, seed, b, noisy,
-                       normals, positions, albedo, clean);
-    return hipGetLastError() == hipSuccess ? BMFR_OK : BMFR_ERROR_HIP;
+    return bmfr_synth_region_device(W, H, 0, 0, W, H, frame, seed, noisy, normals, positions, albedo, clean,
+                                    stream);
 }
 
 }  // extern "C"

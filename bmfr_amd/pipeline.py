@@ -44,6 +44,9 @@ class BmfrConfig:
     position_limit_squared: float = 0.01     # camera_matrices.h, bmfr.cpp:226
     normal_limit_squared: float = 0.1        # camera_matrices.h, bmfr.cpp:227
     use_half_precision_in_tmp_data: int = 1  # bmfr.cpp:88
+    # Multi-GPU tile of the frame (include/bmfr.h: tile_*): (x, y, width, height), halo
+    tile: tuple | None = None
+    tile_halo: int = 0
 
     @property
     def buffer_count(self) -> int:
@@ -65,6 +68,9 @@ class BmfrConfig:
         c.position_limit_squared = self.position_limit_squared
         c.normal_limit_squared = self.normal_limit_squared
         c.use_half_precision_in_tmp_data = self.use_half_precision_in_tmp_data
+        if self.tile is not None:
+            c.tile_x, c.tile_y, c.tile_width, c.tile_height = self.tile
+            c.tile_halo = self.tile_halo
         return c
 
     def sizes(self) -> _lib.Sizes:
@@ -223,9 +229,16 @@ class Denoiser(_Context):
         return p
 
     def copy_output(self, dst: torch.Tensor, stream=None) -> torch.Tensor:
-        """Copy the last frame's TAA output (float3, W*H) into `dst`."""
-        hip_memcpy_d2d(dst.data_ptr(), self.output_ptr(), self.sizes.image_bytes, stream)
+        """Copy the last frame's TAA output (float3 over the buffer region:
+        W*H, or a tile's region) into `dst`."""
+        hip_memcpy_d2d(dst.data_ptr(), self.output_ptr(), self.sizes.region_bytes, stream)
         return dst
+
+    @property
+    def region(self):
+        """(x, y, width, height) of the image pixels this context's planes hold."""
+        s = self.sizes
+        return s.region_x, s.region_y, s.region_width, s.region_height
 
     def copy_state(self, name: str, dst: torch.Tensor, previous: bool = False, stream=None) -> torch.Tensor:
         ptr = getattr(self.state(previous), name)
@@ -266,6 +279,22 @@ def synth_frame_host(width: int, height: int, frame: int, seed: int = 0x424D4652
     check(_lib.load().bmfr_synth_frame_host(width, height, frame, seed, p(out["noisy"]), p(out["normals"]),
                                             p(out["positions"]), p(out["albedo"]),
                                             p(out["clean"]) if clean else None), "bmfr_synth_frame_host")
+    return out
+
+
+def synth_region_device(width: int, height: int, region, frame: int, seed: int = 0x424D4652, device: int = 0,
+                        clean: bool = False, out=None, stream=None):
+    """Render the region (x, y, w, h) of synthetic frame `frame` (a tiled
+    context's inputs) -> dict of float32 tensors (h*w*3), row stride w."""
+    x0, y0, w, h = region
+    dev = torch.device("cuda", device)
+    keys = ("noisy", "normals", "positions", "albedo") + (("clean",) if clean else ())
+    if out is None:
+        out = {k: torch.empty(h * w * 3, dtype=torch.float32, device=dev) for k in keys}
+    check(_lib.load().bmfr_synth_region_device(width, height, x0, y0, w, h, frame, seed, _ptr(out["noisy"]),
+                                               _ptr(out["normals"]), _ptr(out["positions"]),
+                                               _ptr(out["albedo"]), _ptr(out.get("clean")),
+                                               _stream(stream)), "bmfr_synth_region_device")
     return out
 
 

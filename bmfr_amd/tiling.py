@@ -1,0 +1,238 @@
+"""Spatial sharding of a frame over ranks, with the per-frame halo exchange
+(include/bmfr.h tile_*).
+
+Every rank owns one tile of the frame and runs a tiled libbmfr context over
+the tile's *region* (the tile grown by `halo` pixels, clipped to the frame).
+The fused K1 covers the blocks of the frame's shifted block grid that reach
+the tile plus one pixel, so its block fits are the untiled ones; what a rank
+cannot compute itself is the previous frame's temporal state in the halo
+ring, which its neighbours own.  Before each frame > 0, `HaloExchange` moves
+exactly that: for every pair of ranks, the part of the sender's tile that
+lies inside the receiver's region, for the four state planes the next frame
+reads (accumulated noisy colour, spp, accumulated filtered colour, TAA
+output).  Current-frame inputs need no exchange: each rank reads (renders)
+its own region.
+
+Transports: `DistTransport` (torch.distributed point-to-point; RCCL over
+xGMI with the nccl backend, gloo on CPU) and `LoopbackTransport` (all tiles
+in one process -- the single-GPU parity test of the tiled path).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+
+# (plane name in bmfr_state_view, bytes per pixel)
+STATE_PLANES = (("noisy_accumulated", 12), ("spp", 1), ("filtered_accumulated", 12), ("result", 12))
+MIN_HALO = 34  # include/bmfr.h: blocks reach 32 px past the tile, + TAA and bilinear taps
+
+
+def _split(n: int, parts: int, i: int) -> tuple[int, int]:
+    """[start, end) of part i of n split into `parts` near-equal runs, multiples of 32 where possible."""
+    edges = [round(n * k / parts / 32) * 32 for k in range(parts + 1)]
+    edges[-1] = n
+    return edges[i], edges[i + 1]
+
+
+def grid_for(n_ranks: int) -> tuple[int, int]:
+    """Tile grid (columns, rows) for n ranks: 1x1, 2x1, 2x2, 4x2, ..."""
+    tx, ty = 1, 1
+    while tx * ty < n_ranks:
+        if tx <= ty:
+            tx *= 2
+        else:
+            ty *= 2
+    if tx * ty != n_ranks:
+        raise ValueError(f"no power-of-two tile grid for {n_ranks} ranks")
+    return tx, ty
+
+
+Rect = tuple  # (x, y, w, h)
+
+
+def intersect(a: Rect, b: Rect) -> Rect | None:
+    x0, y0 = max(a[0], b[0]), max(a[1], b[1])
+    x1, y1 = min(a[0] + a[2], b[0] + b[2]), min(a[1] + a[3], b[1] + b[3])
+    return (x0, y0, x1 - x0, y1 - y0) if x1 > x0 and y1 > y0 else None
+
+
+@dataclasses.dataclass(frozen=True)
+class TileGrid:
+    """A width x height frame cut into tiles_x x tiles_y tiles (rank = ty * tiles_x + tx)."""
+    width: int
+    height: int
+    tiles_x: int
+    tiles_y: int
+    halo: int = 64
+
+    def __post_init__(self):
+        if self.halo < MIN_HALO:
+            raise ValueError(f"halo must be >= {MIN_HALO}")
+
+    @property
+    def ranks(self) -> int:
+        return self.tiles_x * self.tiles_y
+
+    def tile(self, rank: int) -> Rect:
+        tx, ty = rank % self.tiles_x, rank // self.tiles_x
+        x0, x1 = _split(self.width, self.tiles_x, tx)
+        y0, y1 = _split(self.height, self.tiles_y, ty)
+        return (x0, y0, x1 - x0, y1 - y0)
+
+    def region(self, rank: int) -> Rect:
+        x, y, w, h = self.tile(rank)
+        x0, y0 = max(0, x - self.halo), max(0, y - self.halo)
+        x1, y1 = min(self.width, x + w + self.halo), min(self.height, y + h + self.halo)
+        return (x0, y0, x1 - x0, y1 - y0)
+
+    def plan(self, rank: int):
+        """[(peer, send_rect, recv_rect)]: send the part of my tile inside the
+        peer's region, receive the part of the peer's tile inside mine."""
+        out = []
+        for peer in range(self.ranks):
+            if peer == rank:
+                continue
+            s = intersect(self.tile(rank), self.region(peer))
+            r = intersect(self.tile(peer), self.region(rank))
+            if s or r:
+                out.append((peer, s, r))
+        return out
+
+
+# ---------------------------------------------------------------- copies ----
+class Plane:
+    """A plane of a region-sized buffer: base pointer, region origin/stride, bytes per pixel."""
+
+    def __init__(self, ptr: int, region: Rect, bpp: int):
+        self.ptr, self.region, self.bpp = ptr, region, bpp
+
+    def rect_ptr(self, r: Rect) -> int:
+        return self.ptr + ((r[1] - self.region[1]) * self.region[2] + (r[0] - self.region[0])) * self.bpp
+
+    @property
+    def pitch(self) -> int:
+        return self.region[2] * self.bpp
+
+
+class HipCopier:
+    """Rectangle copies between device planes and flat device buffers (hipMemcpy2DAsync)."""
+
+    def __init__(self, stream=None):
+        self.hip = C.CDLL("libamdhip64.so.7")
+        self.hip.hipMemcpy2DAsync.restype = C.c_int
+        self.hip.hipMemcpy2DAsync.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_size_t,
+                                              C.c_size_t, C.c_int, C.c_void_p]
+        self.stream = stream
+
+    def copy2d(self, dst: int, dpitch: int, src: int, spitch: int, width: int, rows: int) -> None:
+        err = self.hip.hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, 3, self.stream)
+        if err != 0:
+            raise RuntimeError(f"hipMemcpy2DAsync failed: {err}")
+
+
+class HostCopier:
+    """The same on host memory (CPU tests)."""
+
+    def copy2d(self, dst: int, dpitch: int, src: int, spitch: int, width: int, rows: int) -> None:
+        for y in range(rows):
+            C.memmove(dst + y * dpitch, src + y * spitch, width)
+
+
+def pack(copier, planes, rect: Rect, dst: int) -> int:
+    """Copy `rect` of every plane back to back into the flat buffer at dst; returns bytes."""
+    off = 0
+    for p in planes:
+        w = rect[2] * p.bpp
+        copier.copy2d(dst + off, w, p.rect_ptr(rect), p.pitch, w, rect[3])
+        off += w * rect[3]
+    return off
+
+
+def unpack(copier, planes, rect: Rect, src: int) -> int:
+    off = 0
+    for p in planes:
+        w = rect[2] * p.bpp
+        copier.copy2d(p.rect_ptr(rect), p.pitch, src + off, w, w, rect[3])
+        off += w * rect[3]
+    return off
+
+
+def rect_bytes(planes, r: Rect | None) -> int:
+    return 0 if r is None else sum(r[2] * r[3] * p.bpp for p in planes)
+
+
+# ------------------------------------------------------------- transports ----
+class DistTransport:
+    """torch.distributed point-to-point: one grouped batch of isend/irecv per frame."""
+
+    def __init__(self, grid: TileGrid, rank: int, device, host_staging: bool = False):
+        """host_staging: the planes are on a GPU but the process group is gloo
+        (rehearsal of the multi-rank path on one GPU): messages go through host
+        memory."""
+        import torch
+        self.torch = torch
+        self.grid, self.rank, self.device = grid, rank, device
+        self.host_staging = host_staging
+        self._bufs = {}
+
+    def buffer(self, key, nbytes, device=None):
+        b = self._bufs.get(key)
+        if b is None or b.numel() < nbytes:
+            b = self.torch.empty(max(nbytes, 1), dtype=self.torch.uint8, device=device or self.device)
+            self._bufs[key] = b
+        return b
+
+    def exchange(self, planes, copier) -> None:
+        import torch.distributed as dist
+        ops, recvs = [], []
+        cpu = self.torch.device("cpu")
+        for peer, s, r in self.grid.plan(self.rank):
+            if s:
+                n = rect_bytes(planes, s)
+                buf = self.buffer(("s", peer), n)
+                pack(copier, planes, s, buf.data_ptr())
+                if self.host_staging:
+                    self.torch.cuda.synchronize()
+                    sb = self.buffer(("sh", peer), n, cpu)
+                    sb[:n].copy_(buf[:n])
+                    buf = sb
+                ops.append(dist.P2POp(dist.isend, buf[:n], peer))
+            if r:
+                n = rect_bytes(planes, r)
+                buf = self.buffer(("rh" if self.host_staging else "r", peer), n, cpu if self.host_staging else None)
+                ops.append(dist.P2POp(dist.irecv, buf[:n], peer))
+                recvs.append((r, n, buf))
+        if not ops:
+            return
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        for r, n, buf in recvs:
+            if self.host_staging:
+                dbuf = self.buffer(("r", r), n)
+                dbuf[:n].copy_(buf[:n])
+                self.torch.cuda.synchronize()
+                buf = dbuf
+            unpack(copier, planes, r, buf.data_ptr())
+
+
+class LoopbackTransport:
+    """All tiles in one process: copy each peer's tile part straight into my region."""
+
+    def __init__(self, grid: TileGrid):
+        self.grid = grid
+
+    def exchange_all(self, planes_by_rank, copier) -> None:
+        for rank in range(self.grid.ranks):
+            for peer, _, r in self.grid.plan(rank):
+                if not r:
+                    continue
+                for src, dst in zip(planes_by_rank[peer], planes_by_rank[rank]):
+                    w = r[2] * src.bpp
+                    copier.copy2d(dst.rect_ptr(r), dst.pitch, src.rect_ptr(r), src.pitch, w, r[3])
+
+
+def state_planes(denoiser) -> list:
+    """The four exchanged planes of a tiled Denoiser's last frame (the next frame's previous state)."""
+    v = denoiser.state(previous=False)
+    reg = denoiser.region
+    return [Plane(getattr(v, name), reg, bpp) for name, bpp in STATE_PLANES]

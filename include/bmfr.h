@@ -75,9 +75,22 @@ typedef struct bmfr_config {
                                             kernel sees it: float(%g text), bmfr.cpp:226 */
     double normal_limit_squared;         /* idem, bmfr.cpp:227 */
     int use_half_precision_in_tmp_data;  /* USE_HALF_PRECISION_IN_TMP_DATA 1 (bmfr.cpp:88) */
-    /* Spatial tile of a larger frame (multi-GPU sharding); 0/0/0/0 = whole
-     * image.  Tiles use the global block grid and global image borders. */
+    /* Spatial tile of a larger frame (multi-GPU sharding);
+     * 0/0/0/0 = whole image.  image_width/height stay the WHOLE frame: block
+     * grid, mirroring at the borders and reprojection are the whole frame's,
+     * so a tile's output equals the same pixels of the untiled output.  The
+     * context's buffers then cover the tile's REGION = the tile grown by
+     * tile_halo pixels on each side, clipped to the frame (bmfr_sizes
+     * region_*): every plane passed to bmfr_process_frame and every state
+     * plane holds that region with row stride region_width.  Before each
+     * frame > 0 the caller refreshes the region's halo ring of the state
+     * planes (noisy_accumulated, spp, filtered_accumulated, result of
+     * bmfr_state(previous = 0)) from the neighbouring tiles, which own those
+     * pixels.  Exact for scene motion below tile_halo - 34 pixels per frame
+     * (32: blocks reaching past the tile, 2: TAA + bilinear taps).  Canonical
+     * feature lists, fused path only (the stage API rejects tiled contexts). */
     int tile_x, tile_y, tile_width, tile_height;
+    int tile_halo;
 } bmfr_config;
 
 /* Sizes derived from a config (bmfr.cpp:104-118, 316-343). */
@@ -91,6 +104,10 @@ typedef struct bmfr_sizes {
     size_t weights_bytes;   /* bmfr.cpp:338-339 */
     size_t mins_maxs_bytes; /* sized from FEATURES_SCALED (bmfr.cpp:340 assumes 6) */
     size_t image_bytes;     /* one float3 plane, W*H*3*4 */
+    /* Buffer region of the context (the whole frame unless tiled): pixels
+     * [region_x, region_x + region_width) x [region_y, region_y + region_height). */
+    int region_x, region_y, region_width, region_height;
+    size_t region_bytes;    /* one float3 plane of the region */
 } bmfr_sizes;
 
 typedef struct bmfr_ctx bmfr_ctx;
@@ -218,6 +235,11 @@ bmfr_status bmfr_synth_frame_host(int image_width, int image_height, int frame, 
     float *noisy, float *normals, float *positions, float *albedo, float *clean);
 bmfr_status bmfr_synth_frame_device(int image_width, int image_height, int frame, uint32_t seed,
     float *noisy, float *normals, float *positions, float *albedo, float *clean, void *stream);
+/* The region [x0, x0+w) x [y0, y0+h) of the same frame into planes of row
+ * stride w (a tiled context's inputs). */
+bmfr_status bmfr_synth_region_device(int image_width, int image_height, int x0, int y0, int w, int h,
+    int frame, uint32_t seed, float *noisy, float *normals, float *positions, float *albedo, float *clean,
+    void *stream);
 
 #ifdef __cplusplus
 }
