@@ -313,7 +313,11 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
     constexpr int B = NS + FS + 3;
     __shared__ K1Lds<B> L;
     const int t = threadIdx.x;
+#ifdef BMFR_NO_XCD_SWIZZLE
     const int g = blockIdx.x;
+#else
+    const int g = xcd_swizzle(blockIdx.x, gridDim.x);
+#endif
     // Diagnostic build only (-DBMFR_STAMPS): per-block phase timestamps.
 #ifdef BMFR_STAMPS
 #define BMFR_STAMP(k) \

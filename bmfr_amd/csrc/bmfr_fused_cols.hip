@@ -414,7 +414,11 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
     const int t = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int l = t & 63;
+#ifdef BMFR_NO_XCD_SWIZZLE
     const int g = blockIdx.x;
+#else
+    const int g = xcd_swizzle(blockIdx.x, gridDim.x);
+#endif
 #ifdef BMFR_STAMPS
 #define BMFR_STAMP(k) \
     if (t == 0 && stamps) stamps[(size_t)g * 8 + (k)] = __builtin_amdgcn_s_memtime()

@@ -107,6 +107,18 @@ struct Camera {
     float jx, jy;  // this frame's pixel offset
 };
 
+// XCD-aware work-group order.  Work-groups are dealt round-robin to the 8
+// XCDs (g % 8), each with its own L2; renumbering so that XCD x gets the
+// contiguous range [x*G/8, (x+1)*G/8) keeps neighbouring blocks -- which
+// share cache lines of every plane and of the reprojection taps -- on one
+// L2.  A bijection on [0, G) for any G; placement only affects speed.
+__device__ __forceinline__ int xcd_swizzle(int g, int G) {
+    constexpr int kXcds = 8;
+    const int xcd = g % kXcds, k = g / kXcds;
+    const int per = G / kXcds, rem = G % kXcds;
+    return xcd < rem ? xcd * (per + 1) + k : rem * (per + 1) + (xcd - rem) * per + k;
+}
+
 // Linear index of image pixel (x, y) in a plane of the buffer region, and
 // clamps into the region (= the image when untiled).
 __device__ __forceinline__ long pix(const Params& P, int x, int y) {

@@ -168,7 +168,13 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
     const int t = threadIdx.x;
     // Output tile of this launch (the whole image, or a multi-GPU tile whose
     // one-pixel halo lies inside the buffer region).
-    const int x0 = P.tx0 + blockIdx.x * kTaaW, y0 = P.ty0 + blockIdx.y * kTaaH;
+#ifdef BMFR_NO_XCD_SWIZZLE
+    const int bxi = blockIdx.x, byi = blockIdx.y;
+#else
+    const int gi = xcd_swizzle(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    const int bxi = gi % gridDim.x, byi = gi / gridDim.x;
+#endif
+    const int x0 = P.tx0 + bxi * kTaaW, y0 = P.ty0 + byi * kTaaH;
     f3 v[ITER], al[ITER];
 #pragma unroll
     for (int k = 0; k < ITER; ++k) {  // all tile loads in flight first
