@@ -55,11 +55,43 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, varian
     return lib
 
 
+HOST_DIR = os.path.join(HERE, "..", "host")
+IO_LIB = os.path.join(HERE, "libbmfr_io.so")
+HOST_EXE = os.path.join(HERE, "bmfr_host")
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    """Build the host side: libbmfr_io.so (EXR / PNG I/O, host/image_io.cpp)
+    and the bmfr_host program (host/bmfr_host.cpp, the reference's bmfr.cpp
+    on libbmfr), next to libbmfr.so (rpath $ORIGIN)."""
+    build(verbose=verbose)
+    srcs = [os.path.join(HOST_DIR, f) for f in os.listdir(HOST_DIR)]
+    newest = max(os.path.getmtime(f) for f in srcs + [LIB])
+    steps = [
+        (IO_LIB, ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", os.path.join(HOST_DIR, "image_io.cpp"),
+                  "-o", IO_LIB + ".tmp", "-lz"]),
+        (HOST_EXE, [HIPCC, "-O2", "-std=c++17", "-Wall", "-fopenmp", "-I", os.path.join(HERE, "..", "include"),
+                    "-I", HOST_DIR, os.path.join(HOST_DIR, "bmfr_host.cpp"), os.path.join(HOST_DIR, "image_io.cpp"),
+                    "-L", HERE, "-lbmfr", "-lz", "-Wl,-rpath,$ORIGIN", "-o", HOST_EXE + ".tmp"]),
+    ]
+    for out, cmd in steps:
+        if not force and os.path.exists(out) and os.path.getmtime(out) >= newest:
+            continue
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(out + ".tmp", out)
+    return HOST_EXE
+
+
 if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--diag", action="store_true")
     ap.add_argument("--variant", default="")
     ap.add_argument("--flags", default="", help="extra hipcc flags for a variant build")
+    ap.add_argument("--host", action="store_true", help="also build libbmfr_io.so and bmfr_host")
     a = ap.parse_args()
     print(build(force=True, verbose=True, diag=a.diag, variant=a.variant, extra_flags=a.flags.split()))
+    if a.host:
+        print(build_host(force=True, verbose=True))

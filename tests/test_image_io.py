@@ -1,0 +1,218 @@
+"""EXR / PNG I/O of the host (host/image_io.cpp), checked
+against an independent numpy + zlib implementation of the same published
+formats written here: OpenEXR 2 scanline files (HALF / FLOAT channels,
+NONE / RLE / ZIPS / ZIP compression) and 8-bit RGB PNG."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from bmfr_amd import _build
+
+LIB = None
+
+
+def lib():
+    global LIB
+    if LIB is None:
+        _build.build_host()
+        LIB = C.CDLL(_build.IO_LIB)
+        LIB.bmfr_exr_info.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        LIB.bmfr_exr_read_rgb.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_void_p]
+        LIB.bmfr_exr_write_rgb.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t, C.c_int]
+        LIB.bmfr_png_write_rgb.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t]
+        LIB.bmfr_io_error.restype = C.c_char_p
+    return LIB
+
+
+# ---------------------------------------------------- reference encoder ----
+def _attr(name, typ, data):
+    return name.encode() + b"\0" + typ.encode() + b"\0" + struct.pack("<i", len(data)) + data
+
+
+def _predict(raw: bytes) -> bytes:
+    a = np.frombuffer(raw, np.uint8)
+    t = np.concatenate([a[0::2], a[1::2]]).astype(np.int32)
+    d = t.copy()
+    d[1:] = (t[1:] - t[:-1] + 128 + 256) & 255
+    return d.astype(np.uint8).tobytes()
+
+
+def _rle(data: bytes) -> bytes:
+    out, i, n = bytearray(), 0, len(data)
+    while i < n:
+        j = i
+        while j < n and j - i < 127 and data[j] == data[i]:
+            j += 1
+        if j - i >= 3:
+            out += struct.pack("b", j - i - 1) + data[i:i + 1]
+            i = j
+        else:
+            k = i
+            while k < n and k - i < 127 and not (k + 2 < n and data[k] == data[k + 1] == data[k + 2]):
+                k += 1
+            out += struct.pack("b", -(k - i)) + data[i:k]
+            i = k
+    return bytes(out)
+
+
+def write_exr_py(path, img: dict, compression: int, half: bool):
+    """img: channel name -> (H, W) float array.  Channels are stored sorted by name."""
+    names = sorted(img)
+    H, W = img[names[0]].shape
+    ptype, dt = (1, np.float16) if half else (2, np.float32)
+    chl = b"".join(n.encode() + b"\0" + struct.pack("<iIii", ptype, 0, 1, 1) for n in names) + b"\0"
+    box = struct.pack("<iiii", 0, 0, W - 1, H - 1)
+    hdr = (struct.pack("<II", 20000630, 2) + _attr("channels", "chlist", chl) +
+           _attr("compression", "compression", bytes([compression])) + _attr("dataWindow", "box2i", box) +
+           _attr("displayWindow", "box2i", box) + _attr("lineOrder", "lineOrder", b"\0") +
+           _attr("pixelAspectRatio", "float", struct.pack("<f", 1)) +
+           _attr("screenWindowCenter", "v2f", struct.pack("<ff", 0, 0)) +
+           _attr("screenWindowWidth", "float", struct.pack("<f", 1)) + b"\0")
+    lpc = {0: 1, 1: 1, 2: 1, 3: 16}[compression]
+    chunks = []
+    for y0 in range(0, H, lpc):
+        raw = b"".join(np.ascontiguousarray(img[n][y, :]).astype(dt).tobytes()
+                       for y in range(y0, min(H, y0 + lpc)) for n in names)
+        if compression == 1:
+            data = _rle(_predict(raw))
+        elif compression in (2, 3):
+            data = zlib.compress(_predict(raw))
+        else:
+            data = raw
+        if len(data) >= len(raw):
+            data = raw
+        chunks.append(struct.pack("<ii", y0, len(data)) + data)
+    off = len(hdr) + 8 * len(chunks)
+    table = b""
+    for c in chunks:
+        table += struct.pack("<Q", off)
+        off += len(c)
+    with open(path, "wb") as f:
+        f.write(hdr + table + b"".join(chunks))
+
+
+def read_exr_py(path):
+    """Independent decoder for the FLOAT/NONE/ZIP files the host writes."""
+    b = open(path, "rb").read()
+    assert struct.unpack_from("<I", b, 0)[0] == 20000630
+    p, attrs = 8, {}
+    while b[p]:
+        e = b.index(b"\0", p)
+        name = b[p:e].decode()
+        e2 = b.index(b"\0", e + 1)
+        size = struct.unpack_from("<i", b, e2 + 1)[0]
+        attrs[name] = b[e2 + 5:e2 + 5 + size]
+        p = e2 + 5 + size
+    p += 1
+    x0, y0, x1, y1 = struct.unpack("<iiii", attrs["dataWindow"])
+    W, H = x1 - x0 + 1, y1 - y0 + 1
+    comp = attrs["compression"][0]
+    lpc = 16 if comp == 3 else 1
+    n_chunks = (H + lpc - 1) // lpc
+    offs = struct.unpack_from(f"<{n_chunks}Q", b, p)
+    out = np.zeros((H, W, 3), np.float32)
+    for o in offs:
+        y, size = struct.unpack_from("<ii", b, o)
+        data = b[o + 8:o + 8 + size]
+        lines = min(lpc, H - y)
+        raw_size = lines * W * 12
+        if size < raw_size:
+            t = np.frombuffer(zlib.decompress(data), np.uint8).astype(np.int64)
+            t = (t[0] + np.concatenate([[0], np.cumsum(t[1:] - 128)])) & 255  # undo the delta predictor
+            half = (len(t) + 1) // 2
+            r = np.empty(len(t), np.uint8)
+            r[0::2] = t[:half]
+            r[1::2] = t[half:]
+            data = r.tobytes()
+        a = np.frombuffer(data, np.float32).reshape(lines, 3, W)  # B, G, R
+        out[y:y + lines] = a[:, ::-1, :].transpose(0, 2, 1)
+    return out
+
+
+def read_png_py(path):
+    b = open(path, "rb").read()
+    assert b[:8] == b"\x89PNG\r\n\x1a\n"
+    p, idat, W = 8, b"", 0
+    while p < len(b):
+        n = struct.unpack(">I", b[p:p + 4])[0]
+        typ, data = b[p + 4:p + 8], b[p + 8:p + 8 + n]
+        assert zlib.crc32(typ + data) == struct.unpack(">I", b[p + 8 + n:p + 12 + n])[0]
+        if typ == b"IHDR":
+            W, H, depth, ctype = struct.unpack(">IIBB", data[:10])
+            assert (depth, ctype) == (8, 2)
+        elif typ == b"IDAT":
+            idat += data
+        p += 12 + n
+    rows = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(H, 1 + 3 * W)
+    assert (rows[:, 0] == 0).all()
+    return rows[:, 1:].reshape(H, W, 3)
+
+
+def _img(H=37, W=53, seed=1):
+    rng = np.random.default_rng(seed)
+    img = rng.normal(0, 3, (H, W, 3)).astype(np.float32)
+    img[0, 0] = [np.inf, -0.0, 65504.0]
+    img[1, :5, 0] = 0.25  # runs for RLE
+    img[2, :] = 1.0
+    return img
+
+
+# ------------------------------------------------------------------ tests --
+@pytest.mark.parametrize("comp", [0, 3])
+def test_exr_write_read_roundtrip(tmp_path, comp):
+    img = _img()
+    H, W, _ = img.shape
+    path = str(tmp_path / f"rt{comp}.exr").encode()
+    assert lib().bmfr_exr_write_rgb(path, W, H, img.ctypes.data, W * 3, comp) == 0, lib().bmfr_io_error()
+    w, h, c = C.c_int(), C.c_int(), C.c_int()
+    assert lib().bmfr_exr_info(path, C.byref(w), C.byref(h), C.byref(c)) == 0
+    assert (w.value, h.value, c.value) == (W, H, 3)
+    back = np.empty_like(img)
+    assert lib().bmfr_exr_read_rgb(path, W, H, back.ctypes.data) == 0, lib().bmfr_io_error()
+    assert back.tobytes() == img.tobytes()
+    # an independent decoder reads the same values
+    assert read_exr_py(path.decode()).tobytes() == img.tobytes()
+
+
+@pytest.mark.parametrize("comp", [0, 1, 2, 3])
+@pytest.mark.parametrize("half", [False, True])
+def test_exr_reader_against_reference_encoder(tmp_path, comp, half):
+    img = _img(41, 29, seed=comp + 7 * half)
+    chans = {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2], "A": np.ones(img.shape[:2], np.float32)}
+    path = str(tmp_path / f"ref{comp}{int(half)}.exr")
+    write_exr_py(path, chans, comp, half)
+    H, W, _ = img.shape
+    out = np.empty_like(img)
+    assert lib().bmfr_exr_read_rgb(path.encode(), W, H, out.ctypes.data) == 0, lib().bmfr_io_error()
+    want = img.astype(np.float16).astype(np.float32) if half else img
+    np.testing.assert_array_equal(out, want)
+
+
+def test_exr_errors(tmp_path):
+    p = tmp_path / "bad.exr"
+    p.write_bytes(b"not an exr file at all")
+    out = np.empty(3, np.float32)
+    assert lib().bmfr_exr_read_rgb(str(p).encode(), 1, 1, out.ctypes.data) != 0
+    assert b"OpenEXR" in lib().bmfr_io_error()
+    img = _img(8, 8)
+    path = str(tmp_path / "wrongsize.exr").encode()
+    assert lib().bmfr_exr_write_rgb(path, 8, 8, img.ctypes.data, 24, 0) == 0
+    big = np.empty((9, 8, 3), np.float32)
+    assert lib().bmfr_exr_read_rgb(path, 8, 9, big.ctypes.data) != 0
+
+
+def test_png_quantisation(tmp_path):
+    img = _img(23, 31)
+    img[3, 3] = [np.nan, 0.5, 1.5]
+    H, W, _ = img.shape
+    path = str(tmp_path / "o.png").encode()
+    assert lib().bmfr_png_write_rgb(path, W, H, img.ctypes.data, W * 3) == 0, lib().bmfr_io_error()
+    got = read_png_py(path.decode())
+    want = np.floor(np.clip(np.nan_to_num(img, nan=0.0), 0, 1) * 255 + 0.5).astype(np.uint8)
+    np.testing.assert_array_equal(got, want)
