@@ -420,8 +420,11 @@ int run(const Options& o) {
     }
     auto upload = [&](int f) -> hipError_t {
         hipStream_t s = o.pipelined ? copy : compute;
-        if (f >= 2) {  // the slot was last read by frame f-2 (current) and f-1 (previous)
-            hipError_t e = hipStreamWaitEvent(s, consumed[f - 1], 0);
+        // Slot f % 3 was last read by frame f-3 (as current) and frame f-2 (as
+        // previous); upload(f) is issued after frame f-2 was enqueued, so
+        // consumed[f-2] is recorded (an unrecorded event would not be waited on).
+        if (f >= 2) {
+            hipError_t e = hipStreamWaitEvent(s, consumed[f - 2], 0);
             if (e != hipSuccess) return e;
         }
         float** d = dev[f % kRing];
