@@ -105,6 +105,22 @@ __device__ __forceinline__ f3 ycocg_to_rgb(f3 c) {
               dot3(c, f3{0.25f, -0.25f, -0.25f})};
 }
 
+// v_min_f32 / v_max_f32 as written.  fminf / fmaxf on values the compiler
+// cannot prove canonical (loaded from LDS or memory) get a quieting
+// v_max_f32 x, x, x per operand first; the instruction itself already
+// returns the other operand for a quiet NaN, and arithmetic never makes a
+// signalling one, so results are identical for every value reaching here.
+__device__ __forceinline__ float vmin(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 extern "C" __device__ float __ocml_powr_f32(float, float);
 
 // Correctly rounded a / b given y = RN(1/b): one Markstein correction step

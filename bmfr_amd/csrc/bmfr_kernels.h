@@ -591,12 +591,30 @@ __device__ __forceinline__ f3 tone_map(f3 albedo, f3 a) {
               fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.z * a.z), g), 0.f), 1.f)};
 }
 
-// TAA for one pixel (bmfr.cl:873-973).  `ycocg(dx, dy)` returns
-// RGB_to_YCoCg of an in-image neighbour's tone-mapped colour (the centre's is
-// passed as me_y).
-template <class Ycocg>
-__device__ __forceinline__ f3 taa_pixel(const Params& P, int x, int y, f3 me, f3 me_y, float2 pf,
-                                        const float* __restrict__ prev_frame, int frame, Ycocg ycocg) {
+// The four bilinear taps of the previous TAA output at reprojected position
+// pf (bmfr.cl:929-960), loaded unconditionally: the address is clamped in
+// float first, so an off-screen or non-finite pf still reads a valid pixel
+// (taa_resolve then ignores it).  On every path taa_resolve takes, the clamp
+// is the identity and the taps are upstream's.
+__device__ __forceinline__ void taa_load_taps(const Params& P, float2 pf, const float* __restrict__ prev_frame,
+                                              f3 (&pc)[4]) {
+    const int ix = (int)fminf(fmaxf(floorf(pf.x), -2.f), (float)P.width + 1.f);
+    const int iy = (int)fminf(fmaxf(floorf(pf.y), -2.f), (float)P.height + 1.f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        pc[i] = ld3(prev_frame, pix(P, clamp_rx(P, ix + (i & 1)), clamp_ry(P, iy + (i >> 1))));
+}
+
+// TAA for one pixel (bmfr.cl:873-973) given its previous-frame taps (from
+// taa_load_taps) and the YCoCg of its 3x3 neighbourhood in the current
+// tone-mapped frame, nb[3 * (dy + 1) + (dx + 1)] (nb[4] is the centre's).
+// CHECK: skip out-of-image neighbours as upstream does (any value may stand
+// in nb[] for them); without it every neighbour must be in the image.  A
+// skipped neighbour enters the min / max as +inf / -inf, which leaves them
+// unchanged bit for bit, so both forms are upstream's sequence.
+template <bool CHECK>
+__device__ __forceinline__ f3 taa_resolve(const Params& P, int x, int y, f3 me, float2 pf, const f3 (&nb)[9],
+                                          const f3 (&pc)[4], int frame) {
     const int W = P.width, H = P.height;
     const float flx = floorf(pf.x), fly = floorf(pf.y);
     if (frame == 0 || flx < -1.f || fly < -1.f || flx >= (float)W || fly >= (float)H)
@@ -605,30 +623,27 @@ __device__ __forceinline__ f3 taa_pixel(const Params& P, int x, int y, f3 me, f3
     f3 mnb{INFINITY, INFINITY, INFINITY}, mnc = mnb;
     f3 mxb{-INFINITY, -INFINITY, -INFINITY}, mxc = mxb;
 #pragma unroll
-    for (int dy = -1; dy < 2; ++dy)
-#pragma unroll
-        for (int dx = -1; dx < 2; ++dx) {  // bmfr.cl:897-920
+    for (int k = 0; k < 9; ++k) {  // bmfr.cl:897-920, dy outer, dx inner
+        const int dx = k % 3 - 1, dy = k / 3 - 1;
+        f3 lo = nb[k], hi = nb[k];
+        if (CHECK) {
             const int sx = x + dx, sy = y + dy;
-            if (sx >= 0 && sy >= 0 && sx < W && sy < H) {
-                const f3 s = (dx == 0 && dy == 0) ? me_y : ycocg(dx, dy);
-                if (dx == 0 || dy == 0) {
-                    mnc = f3{fminf(mnc.x, s.x), fminf(mnc.y, s.y), fminf(mnc.z, s.z)};
-                    mxc = f3{fmaxf(mxc.x, s.x), fmaxf(mxc.y, s.y), fmaxf(mxc.z, s.z)};
-                }
-                mnb = f3{fminf(mnb.x, s.x), fminf(mnb.y, s.y), fminf(mnb.z, s.z)};
-                mxb = f3{fmaxf(mxb.x, s.x), fmaxf(mxb.y, s.y), fmaxf(mxb.z, s.z)};
-            }
+            const bool in = sx >= 0 && sy >= 0 && sx < W && sy < H;
+            lo = in ? lo : f3{INFINITY, INFINITY, INFINITY};
+            hi = in ? hi : f3{-INFINITY, -INFINITY, -INFINITY};
         }
+        if (dx == 0 || dy == 0) {
+            mnc = f3{vmin(mnc.x, lo.x), vmin(mnc.y, lo.y), vmin(mnc.z, lo.z)};
+            mxc = f3{vmax(mxc.x, hi.x), vmax(mxc.y, hi.y), vmax(mxc.z, hi.z)};
+        }
+        mnb = f3{vmin(mnb.x, lo.x), vmin(mnb.y, lo.y), vmin(mnb.z, lo.z)};
+        mxb = f3{vmax(mxb.x, hi.x), vmax(mxb.y, hi.y), vmax(mxb.z, hi.z)};
+    }
     f3 prev{0.f, 0.f, 0.f};
     float total = 0.f;
     const float fx = pf.x - flx, fy = pf.y - fly;
     const float omx = 1.f - fx, omy = 1.f - fy;
     const float tw[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
-    f3 pc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {  // taps loaded up front (clamped address when skipped)
-        pc[i] = ld3(prev_frame, pix(P, clamp_rx(P, ix + (i & 1)), clamp_ry(P, iy + (i >> 1))));
-    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // bmfr.cl:929-960
         const bool okx = (i & 1) ? (ix < W - 1) : (ix >= 0);

@@ -142,10 +142,13 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
     if (x >= P.width || y >= P.height) return;
     const long lin = (long)y * P.width + x;
     const f3 me = ld3(new_frame, lin);
-    const f3 r = taa_pixel(P, x, y, me, rgb_to_ycocg(me), prev_pixel[lin], prev_frame, frame, [&](int dx, int dy) {
-        return rgb_to_ycocg(ld3(new_frame, lin + (long)dy * P.width + dx));
-    });
-    st3(result, lin, r);
+    const float2 pf = prev_pixel[lin];
+    f3 pc[4], nb[9];
+    taa_load_taps(P, pf, prev_frame, pc);
+#pragma unroll
+    for (int k = 0; k < 9; ++k)  // out-of-image neighbours: a clamped in-image pixel, skipped by taa_resolve
+        nb[k] = rgb_to_ycocg(ld3(new_frame, pix(P, clamp_rx(P, x + k % 3 - 1), clamp_ry(P, y + k / 3 - 1))));
+    st3(result, lin, taa_resolve<true>(P, x, y, me, pf, nb, pc, frame));
 }
 
 // --------------------------------------------------------- fused K2: TAA --
@@ -163,8 +166,8 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
                                                    const float* __restrict__ prev_frame, int frame) {
     constexpr int HW = kTaaW + 2, HH = kTaaH + 2, N = HW * HH;
     constexpr int ITER = (N + 255) / 256;
-    __shared__ float T[3][N];  // RGB
-    __shared__ float Y[3][N];  // YCoCg
+    __shared__ float T[3][N];   // RGB (only the centre's is read)
+    __shared__ float4 Y[N];     // YCoCg (+ pad): one 16-byte read per neighbour
     const int t = threadIdx.x;
     // Output tile of this launch (the whole image, or a multi-GPU tile whose
     // one-pixel halo lies inside the buffer region).
@@ -175,14 +178,33 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
     const int bxi = gi % gridDim.x, byi = gi / gridDim.x;
 #endif
     const int x0 = P.tx0 + bxi * kTaaW, y0 = P.ty0 + byi * kTaaH;
+    // Three dependent round trips per pixel (reprojection -> previous-frame
+    // taps, and the tile) are overlapped: the reprojected positions go out
+    // first, the tile loads behind them, and the taps as soon as the
+    // positions are back -- all before the tile is tone-mapped into LDS.
+    const int tx = t & (kTaaW - 1);
+    float2 pf[kTaaH / 4];
+#pragma unroll
+    for (int k = 0; k < kTaaH / 4; ++k) {
+        const int x = min(x0 + tx, P.tx1 - 1), y = min(y0 + (t >> 6) + 4 * k, P.ty1 - 1);
+        pf[k] = prev_pixel[pix(P, x, y)];
+    }
     f3 v[ITER], al[ITER];
 #pragma unroll
-    for (int k = 0; k < ITER; ++k) {  // all tile loads in flight first
+    for (int k = 0; k < ITER; ++k) {
         const int i = t + 256 * k;
         const int x = min(max(x0 - 1 + i % HW, 0), P.width - 1), y = min(max(y0 - 1 + i / HW, 0), P.height - 1);
         const long lin = pix(P, x, y);
         v[k] = ld3(src, lin);
         if (TONE) al[k] = ld3(albedo, lin);
+    }
+#ifndef BMFR_K2_EARLY_TAPS
+#define BMFR_K2_EARLY_TAPS 1
+#endif
+    f3 taps[kTaaH / 4][4];
+    if constexpr (BMFR_K2_EARLY_TAPS) {
+#pragma unroll
+        for (int k = 0; k < kTaaH / 4; ++k) taa_load_taps(P, pf[k], prev_frame, taps[k]);
     }
 #pragma unroll
     for (int k = 0; k < ITER; ++k) {
@@ -193,19 +215,17 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
             T[0][i] = c.x;
             T[1][i] = c.y;
             T[2][i] = c.z;
-            Y[0][i] = yc.x;
-            Y[1][i] = yc.y;
-            Y[2][i] = yc.z;
+            Y[i] = make_float4(yc.x, yc.y, yc.z, 0.f);
         }
     }
     __syncthreads();
-    const int tx = t & (kTaaW - 1);
-    float2 pf[kTaaH / 4];
+    if constexpr (!BMFR_K2_EARLY_TAPS) {
 #pragma unroll
-    for (int k = 0; k < kTaaH / 4; ++k) {
-        const int x = min(x0 + tx, P.tx1 - 1), y = min(y0 + (t >> 6) + 4 * k, P.ty1 - 1);
-        pf[k] = prev_pixel[pix(P, x, y)];
+        for (int k = 0; k < kTaaH / 4; ++k) taa_load_taps(P, pf[k], prev_frame, taps[k]);
     }
+    // Tiles that reach the image border check every neighbour (bmfr.cl:901);
+    // the others have all nine in the image.
+    const bool edge = x0 == 0 || y0 == 0 || x0 + kTaaW >= P.width || y0 + kTaaH >= P.height;
 #pragma unroll
     for (int k = 0; k < kTaaH / 4; ++k) {
         const int ty = (t >> 6) + 4 * k;
@@ -213,11 +233,14 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
         if (x < P.tx1 && y < P.ty1) {
             const int c = (ty + 1) * HW + tx + 1;
             const f3 me{T[0][c], T[1][c], T[2][c]};
-            const f3 me_y{Y[0][c], Y[1][c], Y[2][c]};
-            const f3 r = taa_pixel(P, x, y, me, me_y, pf[k], prev_frame, frame, [&](int dx, int dy) {
-                const int n = c + dy * HW + dx;
-                return f3{Y[0][n], Y[1][n], Y[2][n]};
-            });
+            f3 nb[9];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                const float4 q = Y[c + (j / 3 - 1) * HW + (j % 3 - 1)];
+                nb[j] = f3{q.x, q.y, q.z};
+            }
+            const f3 r = edge ? taa_resolve<true>(P, x, y, me, pf[k], nb, taps[k], frame)
+                              : taa_resolve<false>(P, x, y, me, pf[k], nb, taps[k], frame);
             st3(result, pix(P, x, y), r);
         }
     }
