@@ -43,14 +43,21 @@ import bmfr_amd  # noqa: E402
 from bmfr_amd import tiling  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# Algorithmic bytes per pixel (SURVEY.md §8d, 18*s + 74 with s = 4 for f32 planes),
-# split over the two kernels by which one touches each compulsory byte:
-#   K1 reads noisy/normal/position (36) + previous normal/position (24)
-#   + accumulated noisy (12) + spp (1) + accumulated filtered (12) and writes
-#   accumulated noisy (12) + spp (1) + accumulated filtered (12) = 110;
-#   K2 reads albedo (12) + the previous TAA output (12), writes the output (12) = 36.
-K1_BYTES_PER_PX = 110
-FRAME_BYTES_PER_PX = 146
+
+
+def k1_bytes_per_px(s: int) -> int:
+    """Algorithmic bytes per pixel (SURVEY.md §8d, 18*s + 74; s = 4 for f32
+    input planes, 2 for half), split over the two kernels by which one
+    touches each compulsory byte.  K1 reads noisy/normal/position (9s) +
+    previous normal/position (6s) + accumulated noisy (12) + spp (1) +
+    accumulated filtered (12) and writes accumulated noisy (12) + spp (1) +
+    accumulated filtered (12): 15s + 50 (110 for f32)."""
+    return 15 * s + 50
+
+
+def frame_bytes_per_px(s: int) -> int:
+    """K1's plus K2's: albedo (3s) + previous TAA output (12) + output (12)."""
+    return 18 * s + 74
 
 
 def parse():
@@ -62,6 +69,9 @@ def parse():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--half-tmp", type=int, default=1)
     ap.add_argument("--third-order", action="store_true", help="B = 16 feature set (BASELINE config 5)")
+    ap.add_argument("--input-half", action="store_true",
+                    help="half3 input planes (BASELINE config 5's fp16 feature buffers)")
+    ap.add_argument("--no-1080p", action="store_true", help="skip the 1920x1080 line (N = 1 only)")
     ap.add_argument("--cpu-frames", type=int, default=2, help="timed CPU-oracle frames (0 = skip)")
     ap.add_argument("--seed", type=int, default=0x424D4652)
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
@@ -113,6 +123,86 @@ def pmc_traffic(workload: str):
     return d.get(workload, {}).get("hbm_bytes_per_launch")
 
 
+def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup):
+    """Denoise frames 0..warmup+steps-1 of the synthetic W x H sequence (this
+    rank's tile of it); time the last `steps` frames.  Returns the timings,
+    per-kernel HIP-event means and the PSNR of the last output."""
+    scaled = bmfr_amd.SCALED_THIRD_ORDER if a.third_order else bmfr_amd.SCALED_DEFAULT
+    cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, scaled=scaled,
+                              use_half_precision_in_tmp_data=a.half_tmp,
+                              tile=tile if grid else None, tile_halo=a.halo if grid else 0,
+                              input_half=int(a.input_half))
+    local = dev.index
+    den = bmfr_amd.Denoiser(cfg, device=local)
+    region = den.region
+    nfr = warmup + steps
+    seed = a.seed
+
+    # Render every frame's region into HBM up front (untimed).
+    frames = [bmfr_amd.synth_region_device(W, H, region, f, seed=seed, device=local) for f in range(nfr)]
+    if a.input_half:  # the planes as half3 (the f32 render rounded to nearest)
+        frames = [{k: (v.half() if k in ("noisy", "normals", "positions", "albedo") else v) for k, v in fr.items()}
+                  for fr in frames]
+    cams = []
+    for f in range(nfr):
+        vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+        _, jit = bmfr_amd.synth_camera(W, H, f)
+        cams.append((vp, jit))
+    transport = tiling.DistTransport(grid, rank, dev, host_staging=backend != "nccl") if grid else None
+    copier = tiling.HipCopier() if grid else None
+    torch.cuda.synchronize()
+
+    def run(f):
+        if transport is not None and f > 0:
+            transport.exchange(tiling.state_planes(den), copier)
+        fr = frames[f]
+        prev = frames[f - 1] if f > 0 else None
+        den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], cams[f][0], cams[f][1], f,
+                          prev_normals=prev["normals"] if prev else None,
+                          prev_positions=prev["positions"] if prev else None)
+
+    for f in range(warmup):
+        run(f)
+    torch.cuda.synchronize()
+    den.set_profiling(True, capacity=max(steps, 1))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for f in range(warmup, nfr):
+        run(f)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = den.profile()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # Quality: PSNR of this rank's tile of the last output against the clean render.
+    clean = bmfr_amd.synth_region_device(W, H, region, nfr - 1, seed=seed, device=local, clean=True)["clean"]
+    out = den.copy_output(torch.empty(region[2] * region[3] * 3, device=dev))
+    torch.cuda.synchronize()
+
+    def tile_of(x):
+        x = x.view(region[3], region[2], 3)
+        return x[tile[1] - region[1]:tile[1] - region[1] + tile[3], tile[0] - region[0]:tile[0] - region[0] + tile[2]]
+
+    last = frames[nfr - 1]
+    noisy_tm = torch.clamp(torch.clamp(last["albedo"].float() * last["noisy"].float(), min=0) ** 0.454545, 0, 1)
+    return {
+        "cfg": cfg,
+        "ms_per_frame": 1e3 * elapsed / steps,
+        "k1_ms": float(np.mean([p[1] for p in prof])),
+        "k2_ms": float(np.mean([p[2] for p in prof])),
+        "dev_ms": float(np.mean([p[3] for p in prof])),
+        "psnr": psnr(tile_of(out).cpu().numpy(), tile_of(clean).cpu().numpy()),
+        "psnr_in": psnr(tile_of(noisy_tm).cpu().numpy(), tile_of(clean).cpu().numpy()),
+    }
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -135,79 +225,21 @@ def main():
     else:
         W, H = a.width, a.height
     grid = tiling.TileGrid(W, H, tx, ty, halo=a.halo) if world > 1 else None
-    scaled = bmfr_amd.SCALED_THIRD_ORDER if a.third_order else bmfr_amd.SCALED_DEFAULT
-    cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, scaled=scaled,
-                              use_half_precision_in_tmp_data=a.half_tmp,
-                              tile=grid.tile(rank) if grid else None, tile_halo=a.halo if grid else 0)
-    den = bmfr_amd.Denoiser(cfg, device=local)
-    region = den.region
     tile = grid.tile(rank) if grid else (0, 0, W, H)
-    nfr = a.warmup + a.steps
-    seed = a.seed
+    r = run_sequence(a, W, H, tile, grid, rank, world, dev, backend, a.steps, a.warmup)
+    cfg = r["cfg"]
+    # The metric's second resolution (BASELINE.json: ms/frame @1080p & 4K), single GPU only.
+    r1080 = None
+    if world == 1 and not a.no_1080p and (W, H) != (1920, 1080):
+        r1080 = run_sequence(a, 1920, 1080, (0, 0, 1920, 1080), None, 0, 1, dev, backend, a.steps, a.warmup)
 
-    # Render every frame's region into HBM up front (untimed).
-    frames = [bmfr_amd.synth_region_device(W, H, region, f, seed=seed, device=local) for f in range(nfr)]
-    cams = []
-    for f in range(nfr):
-        vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
-        _, jit = bmfr_amd.synth_camera(W, H, f)
-        cams.append((vp, jit))
-    transport = tiling.DistTransport(grid, rank, dev, host_staging=backend != "nccl") if grid else None
-    copier = tiling.HipCopier() if grid else None
-    torch.cuda.synchronize()
-
-    def run(f):
-        if transport is not None and f > 0:
-            transport.exchange(tiling.state_planes(den), copier)
-        fr = frames[f]
-        prev = frames[f - 1] if f > 0 else None
-        den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], cams[f][0], cams[f][1], f,
-                          prev_normals=prev["normals"] if prev else None,
-                          prev_positions=prev["positions"] if prev else None)
-
-    for f in range(a.warmup):
-        run(f)
-    torch.cuda.synchronize()
-    den.set_profiling(True, capacity=max(a.steps, 1))
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for f in range(a.warmup, nfr):
-        run(f)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    prof = den.profile()
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    ms_per_frame = 1e3 * elapsed / a.steps
-    k1_ms = float(np.mean([p[1] for p in prof]))
-    k2_ms = float(np.mean([p[2] for p in prof]))
-    dev_ms = float(np.mean([p[3] for p in prof]))
+    s = 2 if a.input_half else 4
     tile_px = tile[2] * tile[3]
-    workload = f"bmfr_{W}x{H}_B{cfg.buffer_count}_{'half' if a.half_tmp else 'f32'}tmp"
-
-    # Quality: PSNR of this rank's tile of the last output against the clean render.
-    clean = bmfr_amd.synth_region_device(W, H, region, nfr - 1, seed=seed, device=local, clean=True)["clean"]
-    out = den.copy_output(torch.empty(region[2] * region[3] * 3, device=dev))
-    torch.cuda.synchronize()
-
-    def tile_of(x):
-        x = x.view(region[3], region[2], 3)
-        return x[tile[1] - region[1]:tile[1] - region[1] + tile[3], tile[0] - region[0]:tile[0] - region[0] + tile[2]]
-
-    q = psnr(tile_of(out).cpu().numpy(), tile_of(clean).cpu().numpy())
-    last = frames[nfr - 1]
-    noisy_tm = torch.clamp(torch.clamp(last["albedo"] * last["noisy"], min=0) ** 0.454545, 0, 1)
-    q_in = psnr(tile_of(noisy_tm).cpu().numpy(), tile_of(clean).cpu().numpy())
-
+    tmp = "half" if a.half_tmp else "f32"
+    workload = f"bmfr_{W}x{H}_B{cfg.buffer_count}_{tmp}tmp" + ("_f16in" if a.input_half else "")
+    ms_per_frame = r["ms_per_frame"]
     if rank == 0:
-        achieved = K1_BYTES_PER_PX * tile_px / (k1_ms * 1e-3) / 1e9
+        achieved = k1_bytes_per_px(s) * tile_px / (r["k1_ms"] * 1e-3) / 1e9
         line = {
             "metric": "ms/frame @1080p & 4K, 1/2/4/8 GPU; PSNR vs 4096spp reference",
             "value": round(ms_per_frame, 4),
@@ -219,24 +251,29 @@ def main():
             "higher_is_better": False,
             "scaling": a.scaling,
             "vs_baseline": None,
-            "dtype": "f32" + ("+f16 tmp_data" if a.half_tmp else ""),
+            "dtype": "f32" + ("+f16 tmp_data" if a.half_tmp else "") + ("+f16 input planes" if a.input_half else ""),
             "data": "synthetic (GPU-rendered 1-spp frames + features, resident in HBM)",
             "config": {"workload": workload, "image": f"{W}x{H}", "buffer_count": cfg.buffer_count,
-                       "half_tmp_data": a.half_tmp, "frames_timed": a.steps,
+                       "half_tmp_data": a.half_tmp, "input_half": int(a.input_half), "frames_timed": a.steps,
                        "parallelism": f"tiles {tx}x{ty}, halo {a.halo} px, RCCL halo exchange" if world > 1
                        else "single GPU"},
-            "device_ms_per_frame": round(dev_ms, 4),
-            "kernel_ms": {"fused_block_k1": round(k1_ms, 4), "taa_k2": round(k2_ms, 4)},
-            "psnr_db": {"output": round(q, 2), "noisy_input": round(q_in, 2)},
+            "device_ms_per_frame": round(r["dev_ms"], 4),
+            "kernel_ms": {"fused_block_k1": round(r["k1_ms"], 4), "taa_k2": round(r["k2_ms"], 4)},
+            "psnr_db": {"output": round(r["psnr"], 2), "noisy_input": round(r["psnr_in"], 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(workload),
                          "kernel": "k_fused_cols (K1)" if a.half_tmp else "k_fused (K1)",
-                         "algorithmic_bytes_per_launch": K1_BYTES_PER_PX * tile_px,
-                         "frame_frac": round(FRAME_BYTES_PER_PX * W * H / (ms_per_frame * 1e-3) / 1e9
+                         "algorithmic_bytes_per_launch": k1_bytes_per_px(s) * tile_px,
+                         "frame_frac": round(frame_bytes_per_px(s) * W * H / (ms_per_frame * 1e-3) / 1e9
                                              / (HBM_PEAK_GBS * world), 4)},
         }
+        if r1080 is not None:
+            line["ms_per_frame_1080p"] = {
+                "value": round(r1080["ms_per_frame"], 4), "device_ms_per_frame": round(r1080["dev_ms"], 4),
+                "kernel_ms": {"fused_block_k1": round(r1080["k1_ms"], 4), "taa_k2": round(r1080["k2_ms"], 4)},
+                "psnr_db": round(r1080["psnr"], 2)}
         if world == 1 and a.cpu_frames > 0:
-            line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_frames, seed)
+            line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_frames, a.seed)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

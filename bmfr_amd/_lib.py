@@ -48,6 +48,7 @@ class Config(C.Structure):
         ("use_half_precision_in_tmp_data", C.c_int),
         ("tile_x", C.c_int), ("tile_y", C.c_int), ("tile_width", C.c_int), ("tile_height", C.c_int),
         ("tile_halo", C.c_int),
+        ("input_half", C.c_int),
     ]
 
 

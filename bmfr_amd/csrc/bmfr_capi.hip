@@ -92,6 +92,8 @@ bmfr_status validate(const bmfr_config* c) {
 }
 
 bool is_tiled(const bmfr_config* c) { return c->tile_width > 0; }
+// The stage kernels take the reference's whole-frame f32 layouts only.
+bool stage_api_ok(const bmfr_config* c) { return !is_tiled(c) && !c->input_half; }
 
 Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     Params P{};
@@ -114,6 +116,7 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     P.position_limit_sq = as_kernel_literal(c->position_limit_squared);
     P.normal_limit_sq = as_kernel_literal(c->normal_limit_squared);
     P.half_tmp = c->use_half_precision_in_tmp_data ? 1 : 0;
+    P.input_half = c->input_half ? 1 : 0;
     // Diagnostic A/B overrides of the fused path: BMFR_FUSED_KERNEL=block
     // (generic-feature K1), k1tone (row-split K1 with tone mapping in K1) or
     // rows (row-split K1, bmfr_fused.hip, instead of the column-split one).
@@ -328,7 +331,7 @@ bmfr_status bmfr_accumulate_noisy_data(bmfr_ctx* c, void* stream, float* out_pre
         !current_noisy || !current_spp || !tmp_data || !prev_frame_camera_matrix || !pixel_offset ||
         frame_number < 0)
         return BMFR_ERROR_INVALID_ARGUMENT;
-    if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // stage kernels use the whole-frame layout
+    if (!stage_api_ok(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
     if (frame_number > 0 && (!previous_normals || !previous_positions || !previous_noisy || !previous_spp))
         return BMFR_ERROR_INVALID_ARGUMENT;
     bmfr::NoisyInputs in{current_normals, previous_normals, current_positions, previous_positions,
@@ -342,7 +345,7 @@ bmfr_status bmfr_accumulate_noisy_data(bmfr_ctx* c, void* stream, float* out_pre
 bmfr_status bmfr_fitter(bmfr_ctx* c, void* stream, float* weights, float* mins_maxs, void* tmp_data,
                         int frame_number) {
     if (!c || !weights || !mins_maxs || !tmp_data || frame_number < 0) return BMFR_ERROR_INVALID_ARGUMENT;
-    if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // stage kernels use the whole-frame layout
+    if (!stage_api_ok(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
     if (!bmfr::fitter_supported(c->P.not_scaled, c->P.scaled)) return BMFR_ERROR_UNSUPPORTED;
     return hip_status(bmfr::launch_fitter(c->P, as_stream(stream), weights, mins_maxs, tmp_data, frame_number));
 }
@@ -354,7 +357,7 @@ bmfr_status bmfr_weighted_sum(bmfr_ctx* c, void* stream, const float* weights, c
     (void)current_noisy;  // debugging-only argument upstream (bmfr.cl:709)
     if (!c || !weights || !mins_maxs || !output || !current_normals || !current_positions || frame_number < 0)
         return BMFR_ERROR_INVALID_ARGUMENT;
-    if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // stage kernels use the whole-frame layout
+    if (!stage_api_ok(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
     return hip_status(bmfr::launch_weighted_sum(c->P, as_stream(stream), weights, mins_maxs, output,
                                                 current_normals, current_positions, frame_number));
 }
@@ -367,7 +370,7 @@ bmfr_status bmfr_accumulate_filtered_data(bmfr_ctx* c, void* stream, const float
     if (!c || !filtered_frame || !in_prev_frame_pixel || !accept_bools || !albedo || !tone_mapped_frame ||
         !current_spp || !accumulated_frame || frame_number < 0)
         return BMFR_ERROR_INVALID_ARGUMENT;
-    if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // stage kernels use the whole-frame layout
+    if (!stage_api_ok(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
     if (frame_number > 0 && !accumulated_prev_frame) return BMFR_ERROR_INVALID_ARGUMENT;
     return hip_status(bmfr::launch_accumulate_filtered(
         c->P, as_stream(stream), filtered_frame, reinterpret_cast<const float2*>(in_prev_frame_pixel),
@@ -379,7 +382,7 @@ bmfr_status bmfr_taa(bmfr_ctx* c, void* stream, const float* in_prev_frame_pixel
                      float* result_frame, const float* prev_frame, int frame_number) {
     if (!c || !in_prev_frame_pixel || !new_frame || !result_frame || frame_number < 0)
         return BMFR_ERROR_INVALID_ARGUMENT;
-    if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // stage kernels use the whole-frame layout
+    if (!stage_api_ok(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
     if (frame_number > 0 && !prev_frame) return BMFR_ERROR_INVALID_ARGUMENT;
     return hip_status(bmfr::launch_taa(c->P, as_stream(stream),
                                        reinterpret_cast<const float2*>(in_prev_frame_pixel), new_frame,
@@ -396,7 +399,7 @@ bmfr_status bmfr_process_frame(bmfr_ctx* c, void* stream, const bmfr_frame_input
     if (frame_number > 0 && (!in->prev_normals || !in->prev_positions || !c->has_frame))
         return BMFR_ERROR_INVALID_ARGUMENT;
     if (!bmfr::fitter_supported(c->P.not_scaled, c->P.scaled)) return BMFR_ERROR_UNSUPPORTED;
-    if (is_tiled(&c->cfg) && !bmfr::fused_supported(c->P)) return BMFR_ERROR_UNSUPPORTED;
+    if ((is_tiled(&c->cfg) || c->cfg.input_half) && !bmfr::fused_supported(c->P)) return BMFR_ERROR_UNSUPPORTED;
     const int cur = c->has_frame ? 1 - c->cur : 0;  // swap, bmfr.cpp:482-484
     const int prv = 1 - cur;
     hipEvent_t* ev = nullptr;
@@ -407,11 +410,14 @@ bmfr_status bmfr_process_frame(bmfr_ctx* c, void* stream, const bmfr_frame_input
         (void)hipEventRecord(ev[0], as_stream(stream));
     }
     bmfr::FusedArgs A;
-    A.in = bmfr::NoisyInputs{in->normals, in->prev_normals, in->positions, in->prev_positions,
-                             in->noisy, c->noisy_acc[prv], c->spp[prv]};
+    // Input planes are float3 or (input_half) half3; the kernels read them
+    // through ld3in<IN> by element type.
+    auto plane = [](const void* p) { return static_cast<const float*>(p); };
+    A.in = bmfr::NoisyInputs{plane(in->normals), plane(in->prev_normals), plane(in->positions),
+                             plane(in->prev_positions), plane(in->noisy), c->noisy_acc[prv], c->spp[prv]};
     A.cam = make_camera(prev_frame_camera_matrix, pixel_offset);
     A.frame = frame_number;
-    A.albedo = in->albedo;
+    A.albedo = plane(in->albedo);
     A.acc_prev = c->acc[prv];
     A.result_prev = c->result[prv];
     A.noisy_out = c->noisy_acc[cur];

@@ -37,6 +37,21 @@ __device__ __forceinline__ void st3(float* __restrict__ b, long i, f3 v) {
     *reinterpret_cast<f3mem*>(b + 3 * i) = f3mem{v.x, v.y, v.z};
 }
 
+// One pixel of an input plane of element type IN (float: the reference's
+// float3 layout; _Float16: half3, 6 bytes per pixel), widened exactly to f32.
+struct __attribute__((packed, aligned(2))) h3mem {
+    _Float16 x, y, z;
+};
+template <class IN>
+__device__ __forceinline__ f3 ld3in(const float* __restrict__ b, long i) {
+    if constexpr (sizeof(IN) == 2) {
+        const h3mem v = reinterpret_cast<const h3mem*>(b)[i];
+        return f3{(float)v.x, (float)v.y, (float)v.z};
+    } else {
+        return ld3(b, i);
+    }
+}
+
 // OpenCL dot() as ROCm's opencl.bc implements it (fmuladd chain).
 __device__ __forceinline__ float dot3(f3 a, f3 b) {
     return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));

@@ -299,7 +299,7 @@ __device__ __forceinline__ void back_substitute(K1Lds<B>& L, int t) {
 #ifndef BMFR_K1_WAVES
 #define BMFR_K1_WAVES 1  // minimum waves per SIMD requested from the register allocator
 #endif
-template <int NS, int FS, bool HALF, bool TONE>
+template <int NS, int FS, bool HALF, bool TONE, class IN>
 __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, NoisyInputs in, Camera cam, int frame,
                                                     const float* __restrict__ albedo,
                                                     float* __restrict__ tone_out,
@@ -335,10 +335,10 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
     NoisyCur cur[kSubs];  // current-frame loads of all four rows go out first
 #pragma unroll
     for (int s = 0; s < kSubs; ++s)
-        cur[s] = noisy_load_current(P, in, bx * kEdge + (t & (kEdge - 1)), by * kEdge + (t >> 5) + 8 * s, frame);
+        cur[s] = noisy_load_current<IN>(P, in, bx * kEdge + (t & (kEdge - 1)), by * kEdge + (t >> 5) + 8 * s, frame);
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {
-        const NoisyItem it = noisy_item_spec(P, in, cam, cur[s], frame);
+        const NoisyItem it = noisy_item_spec<false, IN>(P, in, cam, cur[s], frame);
 #pragma unroll
         for (int f = 0; f < B; ++f) {
             float v;
@@ -428,10 +428,10 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
         const int py = by * kEdge + (t3 >> 5) + 8 * s - kEdge / 2 + off.y;
         // non-owned rows (margins) read a valid pixel and are then skipped
         lin[s] = pix(P, (bits[s] & 1u) ? px : P.ox, (bits[s] & 1u) ? py : P.oy);
-        n[s] = ld3(in.n_cur, lin[s]);
-        pos[s] = ld3(in.p_cur, lin[s]);
+        n[s] = ld3in<IN>(in.n_cur, lin[s]);
+        pos[s] = ld3in<IN>(in.p_cur, lin[s]);
         pp[s] = prev_pixel_out[lin[s]];
-        if (TONE) alb[s] = ld3(albedo, lin[s]);
+        if (TONE) alb[s] = ld3in<IN>(albedo, lin[s]);
     }
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {
@@ -473,21 +473,26 @@ bool fused_supported(const Params& P) {
     return true;
 }
 
-template <int NS, int FS, bool HALF>
+template <int NS, int FS, bool HALF, class IN>
 static void launch_k1(const Params& P, hipStream_t st, const FusedArgs& A) {
     if (k1_tone_maps(P))
-        hipLaunchKernelGGL((k_fused<NS, FS, HALF, true>), dim3(P.nbx * P.nby), dim3(kThreads), 0, st, P,
+        hipLaunchKernelGGL((k_fused<NS, FS, HALF, true, IN>), dim3(P.nbx * P.nby), dim3(kThreads), 0, st, P,
                            A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
                            A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
     else
-    hipLaunchKernelGGL((k_fused<NS, FS, HALF, false>), dim3(P.nbx * P.nby), dim3(kThreads), 0, st, P, A.in,
-                       A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out, A.acc_out,
-                       A.noise_table, A.stamps);
+        hipLaunchKernelGGL((k_fused<NS, FS, HALF, false, IN>), dim3(P.nbx * P.nby), dim3(kThreads), 0, st, P,
+                           A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
+                           A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
+}
+
+template <int FS, bool HALF>
+static void launch_k1_in(const Params& P, hipStream_t st, const FusedArgs& A) {
+    P.input_half ? launch_k1<4, FS, HALF, _Float16>(P, st, A) : launch_k1<4, FS, HALF, float>(P, st, A);
 }
 
 hipError_t launch_fused_k1(const Params& P, hipStream_t st, const FusedArgs& A) {
-    if (P.scaled == 6) P.half_tmp ? launch_k1<4, 6, true>(P, st, A) : launch_k1<4, 6, false>(P, st, A);
-    else P.half_tmp ? launch_k1<4, 9, true>(P, st, A) : launch_k1<4, 9, false>(P, st, A);
+    if (P.scaled == 6) P.half_tmp ? launch_k1_in<6, true>(P, st, A) : launch_k1_in<6, false>(P, st, A);
+    else P.half_tmp ? launch_k1_in<9, true>(P, st, A) : launch_k1_in<9, false>(P, st, A);
     return hipGetLastError();
 }
 

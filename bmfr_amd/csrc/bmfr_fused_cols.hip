@@ -400,7 +400,7 @@ __device__ __forceinline__ void back_substitute(Lds<B>& L, int t) {
 #ifndef BMFR_COLS_WAVES
 #define BMFR_COLS_WAVES 1  // minimum waves per SIMD requested from the register allocator
 #endif
-template <int NS, int FS>
+template <int NS, int FS, class IN>
 __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params P, NoisyInputs in, Camera cam, int frame,
                                                           const float* __restrict__ acc_prev,
                                                           float* __restrict__ noisy_out,
@@ -445,11 +445,11 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
         NoisyCur cur[PB];
 #pragma unroll
         for (int k = 0; k < PB; ++k)
-            cur[k] = noisy_load_current(P, in, bx * kEdge + lx, by * kEdge + ly + 2 * (i0 + k), frame);
+            cur[k] = noisy_load_current<IN>(P, in, bx * kEdge + lx, by * kEdge + ly + 2 * (i0 + k), frame);
 #pragma unroll
         for (int k = 0; k < PB; ++k) {
             const int i = i0 + k;
-            const NoisyItem it = noisy_item_spec<true>(P, in, cam, cur[k], frame, acc_prev);
+            const NoisyItem it = noisy_item_spec<true, IN>(P, in, cam, cur[k], frame, acc_prev);
 #pragma unroll
             for (int f = 1; f < B; ++f) {
                 float v;
@@ -528,8 +528,8 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
         const int px = bx * kEdge + (l3 & (kEdge - 1)) - kEdge / 2 + off.x;
         const int py = by * kEdge + (l3 >> 5) + 8 * w + 2 * i - kEdge / 2 + off.y;
         lin[i] = pix(P, (ibits & (1u << i)) ? px : P.ox, (ibits & (1u << i)) ? py : P.oy);  // margins: a valid pixel, skipped below
-        nrm[i] = ld3(in.n_cur, lin[i]);
-        wp[i] = ld3(in.p_cur, lin[i]);
+        nrm[i] = ld3in<IN>(in.n_cur, lin[i]);
+        wp[i] = ld3in<IN>(in.p_cur, lin[i]);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -575,14 +575,16 @@ bool fused_cols_supported(const Params& P) {
     return P.half_tmp && P.fused_variant == 0 && fused_supported(P);
 }
 
+template <int FS, class IN>
+static void launch_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
+    hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN>), dim3(P.nbx * P.nby), dim3(cols::kThreads), 0, st, P, A.in,
+                       A.cam, A.frame, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out, A.acc_out,
+                       A.noise_table, A.stamps);
+}
+
 hipError_t launch_fused_k1_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
-    const dim3 grid(P.nbx * P.nby), block(cols::kThreads);
-    if (P.scaled == 6)
-        hipLaunchKernelGGL((cols::k_fused_cols<4, 6>), grid, block, 0, st, P, A.in, A.cam, A.frame, A.acc_prev,
-                           A.noisy_out, A.spp_out, A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
-    else
-        hipLaunchKernelGGL((cols::k_fused_cols<4, 9>), grid, block, 0, st, P, A.in, A.cam, A.frame, A.acc_prev,
-                           A.noisy_out, A.spp_out, A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
+    if (P.scaled == 6) P.input_half ? launch_cols<6, _Float16>(P, st, A) : launch_cols<6, float>(P, st, A);
+    else P.input_half ? launch_cols<9, _Float16>(P, st, A) : launch_cols<9, float>(P, st, A);
     return hipGetLastError();
 }
 

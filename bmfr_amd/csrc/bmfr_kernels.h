@@ -222,6 +222,7 @@ struct NoisyCur {
     int px, py;
     bool owner;
 };
+template <class IN = float>
 __device__ __forceinline__ NoisyCur noisy_load_current(const Params& P, const NoisyInputs& in, int gx, int gy,
                                                        int frame) {
     NoisyCur c;
@@ -231,13 +232,13 @@ __device__ __forceinline__ NoisyCur noisy_load_current(const Params& P, const No
     c.py = mirror(uy, P.height);
     c.owner = ux >= 0 && ux < P.width && uy >= 0 && uy < P.height;
     const long lin = pix(P, c.px, c.py);
-    c.wp = ld3(in.p_cur, lin);
-    c.nrm = ld3(in.n_cur, lin);
-    c.cur = ld3(in.noisy_cur, lin);
+    c.wp = ld3in<IN>(in.p_cur, lin);
+    c.nrm = ld3in<IN>(in.n_cur, lin);
+    c.cur = ld3in<IN>(in.noisy_cur, lin);
     return c;
 }
 
-template <bool FILT = false>
+template <bool FILT = false, class IN = float>
 __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const NoisyInputs& in, const Camera& cam,
                                                      const NoisyCur& c, int frame,
                                                      const float* __restrict__ acc_prev = nullptr) {
@@ -285,8 +286,8 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
             const int sx = ix + (i & 1), sy = iy + (i >> 1);
             inb[i] = sx >= 0 && sy >= 0 && sx < P.width && sy < P.height;
             const long s = pix(P, clamp_rx(P, sx), clamp_ry(P, sy));
-            pp[i] = ld3(in.p_prev, s);
-            pn[i] = ld3(in.n_prev, s);
+            pp[i] = ld3in<IN>(in.p_prev, s);
+            pn[i] = ld3in<IN>(in.n_prev, s);
             pc[i] = ld3(in.noisy_prev, s);
             sp[i] = (float)in.spp_prev[s];
             if (FILT) pa[i] = ld3(acc_prev, s);  // same taps (bmfr.cl:801-832)

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
 // tone-mapped here from the accumulated colour and the albedo (K1 then
 // writes no tone-mapped frame); otherwise K1's tone-mapped frame is read.
 constexpr int kTaaW = 64, kTaaH = 16;
-template <bool TONE>
+template <bool TONE, class IN>
 __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __restrict__ src,
                                                    const float* __restrict__ albedo,
                                                    const float2* __restrict__ prev_pixel,
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
         const int x = min(max(x0 - 1 + i % HW, 0), P.width - 1), y = min(max(y0 - 1 + i / HW, 0), P.height - 1);
         const long lin = pix(P, x, y);
         v[k] = ld3(src, lin);
-        if (TONE) al[k] = ld3(albedo, lin);
+        if (TONE) al[k] = ld3in<IN>(albedo, lin);
     }
 #ifndef BMFR_K2_EARLY_TAPS
 #define BMFR_K2_EARLY_TAPS 1
@@ -410,10 +410,13 @@ hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& 
         if (mid) (void)hipEventRecord(mid, st);
         const dim3 grd((P.tx1 - P.tx0 + kTaaW - 1) / kTaaW, (P.ty1 - P.ty0 + kTaaH - 1) / kTaaH);
         if (k1_tone_maps(P))
-            hipLaunchKernelGGL(k_fused_taa<false>, grd, dim3(256), 0, st, P, A.tone_out, A.albedo,
+            hipLaunchKernelGGL((k_fused_taa<false, float>), grd, dim3(256), 0, st, P, A.tone_out, A.albedo,
+                               A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
+        else if (P.input_half)
+            hipLaunchKernelGGL((k_fused_taa<true, _Float16>), grd, dim3(256), 0, st, P, A.acc_out, A.albedo,
                                A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
         else
-            hipLaunchKernelGGL(k_fused_taa<true>, grd, dim3(256), 0, st, P, A.acc_out, A.albedo,
+            hipLaunchKernelGGL((k_fused_taa<true, float>), grd, dim3(256), 0, st, P, A.acc_out, A.albedo,
                                A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
         return hipGetLastError();
     }

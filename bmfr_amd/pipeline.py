@@ -47,6 +47,8 @@ class BmfrConfig:
     # Multi-GPU tile of the frame (include/bmfr.h: tile_*): (x, y, width, height), halo
     tile: tuple | None = None
     tile_halo: int = 0
+    # Frame input planes in IEEE half (half3, 6 B/px) instead of f32 (include/bmfr.h: input_half)
+    input_half: int = 0
 
     @property
     def buffer_count(self) -> int:
@@ -71,6 +73,7 @@ class BmfrConfig:
         if self.tile is not None:
             c.tile_x, c.tile_y, c.tile_width, c.tile_height = self.tile
             c.tile_halo = self.tile_halo
+        c.input_half = self.input_half
         return c
 
     def sizes(self) -> _lib.Sizes:

@@ -91,6 +91,14 @@ typedef struct bmfr_config {
      * feature lists, fused path only (the stage API rejects tiled contexts). */
     int tile_x, tile_y, tile_width, tile_height;
     int tile_halo;
+    /* Input planes of bmfr_process_frame (noisy, normals, positions, albedo
+     * and the previous normals / positions) in IEEE half, interleaved RGB
+     * (6 bytes per pixel), instead of f32: the .exr files' own HALF channels
+     * kept as they are (the reference converts them to FLOAT on load,
+     * bmfr.cpp:157-159).  Values are widened exactly to f32 on load, so the
+     * output equals the f32 path's on the widened planes bit for bit.
+     * Canonical feature lists, fused path only (stage API: unsupported). */
+    int input_half;
 } bmfr_config;
 
 /* Sizes derived from a config (bmfr.cpp:104-118, 316-343). */
@@ -168,13 +176,13 @@ bmfr_status bmfr_taa(bmfr_ctx *ctx, void *stream, const float *in_prev_frame_pix
  * keeps, bmfr.cpp:316-319).  Temporal state (accumulated noisy colour, spp,
  * accumulated filtered colour, TAA output) lives in the context and is
  * double-buffered and swapped per frame like bmfr.cpp:482-484. */
-typedef struct bmfr_frame_inputs {
-    const float *noisy;           /* 1-spp colour (demodulated), float3 */
-    const float *normals;         /* shading normals, float3 */
-    const float *positions;       /* world positions, float3 */
-    const float *albedo;          /* float3 */
-    const float *prev_normals;    /* previous frame's normals (ignored at frame 0) */
-    const float *prev_positions;  /* previous frame's positions (ignored at frame 0) */
+typedef struct bmfr_frame_inputs {  /* float3 planes, or half3 with input_half */
+    const void *noisy;           /* 1-spp colour (demodulated) */
+    const void *normals;         /* shading normals */
+    const void *positions;       /* world positions */
+    const void *albedo;
+    const void *prev_normals;    /* previous frame's normals (ignored at frame 0) */
+    const void *prev_positions;  /* previous frame's positions (ignored at frame 0) */
 } bmfr_frame_inputs;
 
 /* prev_frame_camera_matrix: column-major view-projection of frame-1
