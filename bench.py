@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="multi-GPU: weak = one --width x --height tile per GPU, strong = one frame split")
     ap.add_argument("--halo", type=int, default=64, help="tile halo in pixels (>= 34 + max motion)")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false",
+                    help="multi-GPU: exchange the halo before the frame instead of under K1's interior blocks")
     return ap.parse_args()
 
 
@@ -149,17 +151,35 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup):
         _, jit = bmfr_amd.synth_camera(W, H, f)
         cams.append((vp, jit))
     transport = tiling.DistTransport(grid, rank, dev, host_staging=backend != "nccl") if grid else None
-    copier = tiling.HipCopier() if grid else None
+    # Tiled: the halo exchange runs on its own stream while K1's interior
+    # blocks (which need no halo) run on the compute stream
+    # (bmfr_process_frame_interior / _border, include/bmfr.h).
+    compute = torch.cuda.current_stream(dev)
+    comm = torch.cuda.Stream(dev) if grid else None
+    copier = tiling.HipCopier(stream=comm.cuda_stream if (grid and a.overlap) else None) if grid else None
+    frame_done = torch.cuda.Event() if grid else None
     torch.cuda.synchronize()
 
     def run(f):
-        if transport is not None and f > 0:
-            transport.exchange(tiling.state_planes(den), copier)
         fr = frames[f]
         prev = frames[f - 1] if f > 0 else None
-        den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], cams[f][0], cams[f][1], f,
-                          prev_normals=prev["normals"] if prev else None,
-                          prev_positions=prev["positions"] if prev else None)
+        args = (fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], cams[f][0], cams[f][1], f)
+        kw = dict(prev_normals=prev["normals"] if prev else None, prev_positions=prev["positions"] if prev else None)
+        if transport is None or f == 0:
+            den.process_frame(*args, **kw)
+        elif not a.overlap:
+            transport.exchange(tiling.state_planes(den), copier)
+            den.process_frame(*args, **kw)
+        else:
+            planes = tiling.state_planes(den)  # the previous frame's state until _border
+            comm.wait_event(frame_done)
+            den.process_frame_interior(*args, **kw)
+            with torch.cuda.stream(comm):
+                transport.exchange(planes, copier)
+            compute.wait_stream(comm)
+            den.process_frame_border(*args, **kw)
+        if frame_done is not None:
+            frame_done.record(compute)
 
     for f in range(warmup):
         run(f)
@@ -255,13 +275,16 @@ def main():
             "data": "synthetic (GPU-rendered 1-spp frames + features, resident in HBM)",
             "config": {"workload": workload, "image": f"{W}x{H}", "buffer_count": cfg.buffer_count,
                        "half_tmp_data": a.half_tmp, "input_half": int(a.input_half), "frames_timed": a.steps,
-                       "parallelism": f"tiles {tx}x{ty}, halo {a.halo} px, RCCL halo exchange" if world > 1
-                       else "single GPU"},
+                       "parallelism": (f"tiles {tx}x{ty}, halo {a.halo} px, "
+                                       f"{'RCCL' if backend == 'nccl' else backend} halo exchange"
+                                       f"{' overlapped with interior blocks' if a.overlap else ''}")
+                       if world > 1 else "single GPU"},
             "device_ms_per_frame": round(r["dev_ms"], 4),
             "kernel_ms": {"fused_block_k1": round(r["k1_ms"], 4), "taa_k2": round(r["k2_ms"], 4)},
             "psnr_db": {"output": round(r["psnr"], 2), "noisy_input": round(r["psnr_in"], 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(workload),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": pmc_traffic(workload) if world == 1 else None,
                          "kernel": "k_fused_cols (K1)" if a.half_tmp else "k_fused (K1)",
                          "algorithmic_bytes_per_launch": k1_bytes_per_px(s) * tile_px,
                          "frame_frac": round(frame_bytes_per_px(s) * W * H / (ms_per_frame * 1e-3) / 1e9

@@ -98,6 +98,8 @@ SIGNATURES = {
     "bmfr_accumulate_filtered_data": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I]),
     "bmfr_taa": (_I, [_P, _P, _P, _P, _P, _P, _I]),
     "bmfr_process_frame": (_I, [_P, _P, C.POINTER(FrameInputs), _F16, _F2, _I]),
+    "bmfr_process_frame_interior": (_I, [_P, _P, C.POINTER(FrameInputs), _F16, _F2, _I]),
+    "bmfr_process_frame_border": (_I, [_P, _P, C.POINTER(FrameInputs), _F16, _F2, _I]),
     "bmfr_output": (_P, [_P]),
     "bmfr_state": (_I, [_P, _I, C.POINTER(StateView)]),
     "bmfr_set_profiling": (_I, [_P, _I, _I]),

@@ -32,6 +32,8 @@ struct bmfr_ctx {
     unsigned long long* stamps = nullptr;  // diagnostic: BMFR_STAMPS=1 with libbmfr_diag.so
     int cur = 0;
     bool has_frame = false;
+    // bmfr_process_frame_interior issued for this frame, border part pending
+    int pending_frame = -1;
     // Profiling ring: 3 events per frame (before K1, after K1, after K2).
     int prof_capacity = 0;
     long prof_count = 0;
@@ -390,32 +392,30 @@ bmfr_status bmfr_taa(bmfr_ctx* c, void* stream, const float* in_prev_frame_pixel
 }
 
 // ----------------------------------------------------------- frame API ----
-bmfr_status bmfr_process_frame(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
-                               const float prev_frame_camera_matrix[16], const float pixel_offset[2],
-                               int frame_number) {
-    if (!c || !in || !in->noisy || !in->normals || !in->positions || !in->albedo ||
-        !prev_frame_camera_matrix || !pixel_offset || frame_number < 0)
+namespace {
+
+bmfr_status check_frame_args(const bmfr_ctx* c, const bmfr_frame_inputs* in, const float* m, const float* off,
+                             int frame_number) {
+    if (!c || !in || !in->noisy || !in->normals || !in->positions || !in->albedo || !m || !off || frame_number < 0)
         return BMFR_ERROR_INVALID_ARGUMENT;
     if (frame_number > 0 && (!in->prev_normals || !in->prev_positions || !c->has_frame))
         return BMFR_ERROR_INVALID_ARGUMENT;
     if (!bmfr::fitter_supported(c->P.not_scaled, c->P.scaled)) return BMFR_ERROR_UNSUPPORTED;
     if ((is_tiled(&c->cfg) || c->cfg.input_half) && !bmfr::fused_supported(c->P)) return BMFR_ERROR_UNSUPPORTED;
-    const int cur = c->has_frame ? 1 - c->cur : 0;  // swap, bmfr.cpp:482-484
+    return BMFR_OK;
+}
+
+// The kernels' arguments for frame `frame_number`, writing state slot `cur`.
+bmfr::FusedArgs frame_args(const bmfr_ctx* c, const bmfr_frame_inputs* in, const float* m, const float* off,
+                           int frame_number, int cur) {
     const int prv = 1 - cur;
-    hipEvent_t* ev = nullptr;
-    if (c->prof_capacity > 0) {
-        const int slot = (int)(c->prof_count % c->prof_capacity);
-        ev = c->prof_events + 3 * slot;
-        c->prof_frames[slot] = frame_number;
-        (void)hipEventRecord(ev[0], as_stream(stream));
-    }
     bmfr::FusedArgs A;
     // Input planes are float3 or (input_half) half3; the kernels read them
     // through ld3in<IN> by element type.
     auto plane = [](const void* p) { return static_cast<const float*>(p); };
     A.in = bmfr::NoisyInputs{plane(in->normals), plane(in->prev_normals), plane(in->positions),
                              plane(in->prev_positions), plane(in->noisy), c->noisy_acc[prv], c->spp[prv]};
-    A.cam = make_camera(prev_frame_camera_matrix, pixel_offset);
+    A.cam = make_camera(m, off);
     A.frame = frame_number;
     A.albedo = plane(in->albedo);
     A.acc_prev = c->acc[prv];
@@ -428,16 +428,125 @@ bmfr_status bmfr_process_frame(bmfr_ctx* c, void* stream, const bmfr_frame_input
     A.result_out = c->result[cur];
     A.noise_table = c->noise_table;
     A.stamps = c->stamps;
-    const bmfr_status st =
-        hip_status(bmfr::launch_fused_frame(frame_params(c, frame_number), as_stream(stream), A, ev ? ev[1] : nullptr));
+    return A;
+}
+
+// Blocks of frame `frame`'s K1 launch (frame_params) whose reads of the
+// previous frame's state stay inside the tile: every pixel of the block
+// (mirrored at the frame border, bmfr.cl:310-317) plus the reprojection
+// reach -- tile_halo - 34 pixels of motion (include/bmfr.h) and one more for
+// the bilinear taps -- clipped to the frame lies in the tile.  Those blocks
+// need no halo; they form a rectangle [*i0, *i1) of block indices per axis
+// (empty when i0 == i1).  Untiled contexts: every block.
+void interior_blocks(const bmfr_ctx* c, const Params& P, int frame, int* ix0, int* ix1, int* iy0, int* iy1) {
+    const bmfr_config& g = c->cfg;
+    if (!is_tiled(&g)) {
+        *ix0 = P.bx0, *ix1 = P.bx0 + P.nbx, *iy0 = P.by0, *iy1 = P.by0 + P.nby;
+        return;
+    }
+    const int E = BMFR_BLOCK_EDGE_LENGTH, reach = g.tile_halo - 33;
+    auto axis = [&](int b0, int nb, int off, int size, int t0, int t1, int* i0, int* i1) {
+        *i0 = *i1 = b0;
+        int first = -1, last = -1;
+        for (int b = b0; b < b0 + nb; ++b) {
+            int lo = size, hi = -1;
+            for (int p = E * b - E / 2 + off; p < E * b + E / 2 + off; ++p) {
+                const int m = p < 0 ? -p - 1 : (p >= size ? 2 * size - p - 1 : p);
+                lo = std::min(lo, m);
+                hi = std::max(hi, m);
+            }
+            const bool in = std::max(lo - reach, 0) >= t0 && std::min(hi + reach, size - 1) < t1;
+            if (in) {
+                if (first < 0) first = b;
+                if (last >= 0 && last != b - 1) return;  // not one run: treat all as border
+                last = b;
+            }
+        }
+        if (first >= 0) *i0 = first, *i1 = last + 1;
+    };
+    const int ox = bmfr::kBlockOffsetTable[frame & 15][0], oy = bmfr::kBlockOffsetTable[frame & 15][1];
+    axis(P.bx0, P.nbx, ox, g.image_width, g.tile_x, g.tile_x + g.tile_width, ix0, ix1);
+    axis(P.by0, P.nby, oy, g.image_height, g.tile_y, g.tile_y + g.tile_height, iy0, iy1);
+    if (*ix0 == *ix1 || *iy0 == *iy1) *ix0 = *ix1 = P.bx0, *iy0 = *iy1 = P.by0;
+}
+
+Params block_rect(Params P, int x0, int x1, int y0, int y1) {
+    P.bx0 = x0;
+    P.nbx = x1 - x0;
+    P.by0 = y0;
+    P.nby = y1 - y0;
+    return P;
+}
+
+// PART 0: noise table + interior blocks.  PART 1: border blocks + K2 (+ swap).
+// PART 2: everything (bmfr_process_frame).
+bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in, const float* m,
+                         const float* off, int frame_number, int part) {
+    bmfr_status st = check_frame_args(c, in, m, off, frame_number);
     if (st != BMFR_OK) return st;
-    if (ev) {
-        (void)hipEventRecord(ev[2], as_stream(stream));
+    if (part == 1 && c->pending_frame != frame_number) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (part != 1 && c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
+    const hipStream_t s = as_stream(stream);
+    const int cur = c->has_frame ? 1 - c->cur : 0;  // swap, bmfr.cpp:482-484
+    const bmfr::FusedArgs A = frame_args(c, in, m, off, frame_number, cur);
+    const Params P = frame_params(c, frame_number);
+    if (part != 2 && !bmfr::fused_supported(P)) return BMFR_ERROR_UNSUPPORTED;
+    hipEvent_t* ev = nullptr;
+    if (c->prof_capacity > 0) {
+        const long n = part == 1 ? c->prof_count - 1 : c->prof_count;
+        ev = c->prof_events + 3 * (int)(n % c->prof_capacity);
+    }
+    if (part != 1 && ev) {
+        c->prof_frames[(int)(c->prof_count % c->prof_capacity)] = frame_number;
+        (void)hipEventRecord(ev[0], s);
         ++c->prof_count;
     }
+    if (part == 2) {
+        st = hip_status(bmfr::launch_fused_frame(P, s, A, ev ? ev[1] : nullptr));
+        if (st != BMFR_OK) return st;
+    } else {
+        int ix0, ix1, iy0, iy1;
+        interior_blocks(c, P, frame_number, &ix0, &ix1, &iy0, &iy1);
+        if (part == 0) {
+            if ((st = hip_status(bmfr::launch_noise_table(P, s, A))) != BMFR_OK) return st;
+            st = hip_status(bmfr::launch_fused_k1_blocks(block_rect(P, ix0, ix1, iy0, iy1), s, A));
+            if (st != BMFR_OK) return st;
+            c->pending_frame = frame_number;
+            return BMFR_OK;
+        }
+        const int x0 = P.bx0, x1 = P.bx0 + P.nbx, y0 = P.by0, y1 = P.by0 + P.nby;
+        const Params strips[4] = {block_rect(P, x0, x1, y0, iy0), block_rect(P, x0, x1, iy1, y1),
+                                  block_rect(P, x0, ix0, iy0, iy1), block_rect(P, ix1, x1, iy0, iy1)};
+        for (const Params& S : strips)  // an empty interior leaves the whole launch in strips[0]
+            if ((st = hip_status(bmfr::launch_fused_k1_blocks(S, s, A))) != BMFR_OK) return st;
+        if (ev) (void)hipEventRecord(ev[1], s);
+        if ((st = hip_status(bmfr::launch_fused_k2(P, s, A))) != BMFR_OK) return st;
+        c->pending_frame = -1;
+    }
+    if (ev) (void)hipEventRecord(ev[2], s);
     c->cur = cur;
     c->has_frame = true;
     return BMFR_OK;
+}
+
+}  // namespace
+
+bmfr_status bmfr_process_frame(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
+                               const float prev_frame_camera_matrix[16], const float pixel_offset[2],
+                               int frame_number) {
+    return process_part(c, stream, in, prev_frame_camera_matrix, pixel_offset, frame_number, 2);
+}
+
+bmfr_status bmfr_process_frame_interior(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
+                                        const float prev_frame_camera_matrix[16], const float pixel_offset[2],
+                                        int frame_number) {
+    return process_part(c, stream, in, prev_frame_camera_matrix, pixel_offset, frame_number, 0);
+}
+
+bmfr_status bmfr_process_frame_border(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
+                                      const float prev_frame_camera_matrix[16], const float pixel_offset[2],
+                                      int frame_number) {
+    return process_part(c, stream, in, prev_frame_camera_matrix, pixel_offset, frame_number, 1);
 }
 
 bmfr_status bmfr_set_profiling(bmfr_ctx* c, int enable, int capacity) {

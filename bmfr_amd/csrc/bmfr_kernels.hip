@@ -399,26 +399,39 @@ static hipError_t launch_fused_t(const Params& P, hipStream_t st, const FusedArg
     return hipGetLastError();
 }
 
+hipError_t launch_noise_table(const Params& P, hipStream_t st, const FusedArgs& A) {
+    const int n = (P.buffers - 4) * kBlockPixels;
+    hipLaunchKernelGGL(k_noise_table, dim3((n + 255) / 256), dim3(256), 0, st, A.frame, P.buffers, P.noise2,
+                       A.noise_table);
+    return hipGetLastError();
+}
+
+hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedArgs& A) {
+    if (P.nbx <= 0 || P.nby <= 0) return hipSuccess;
+    return fused_cols_supported(P) ? launch_fused_k1_cols(P, st, A) : launch_fused_k1(P, st, A);
+}
+
+hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A) {
+    const dim3 grd((P.tx1 - P.tx0 + kTaaW - 1) / kTaaW, (P.ty1 - P.ty0 + kTaaH - 1) / kTaaH);
+    if (k1_tone_maps(P))
+        hipLaunchKernelGGL((k_fused_taa<false, float>), grd, dim3(256), 0, st, P, A.tone_out, A.albedo,
+                           A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
+    else if (P.input_half)
+        hipLaunchKernelGGL((k_fused_taa<true, _Float16>), grd, dim3(256), 0, st, P, A.acc_out, A.albedo,
+                           A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
+    else
+        hipLaunchKernelGGL((k_fused_taa<true, float>), grd, dim3(256), 0, st, P, A.acc_out, A.albedo,
+                           A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
+    return hipGetLastError();
+}
+
 hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& A, hipEvent_t mid) {
     hipError_t e;
     if (fused_supported(P)) {
-        const int n = (P.buffers - 4) * kBlockPixels;
-        hipLaunchKernelGGL(k_noise_table, dim3((n + 255) / 256), dim3(256), 0, st, A.frame, P.buffers, P.noise2,
-                           A.noise_table);
-        e = fused_cols_supported(P) ? launch_fused_k1_cols(P, st, A) : launch_fused_k1(P, st, A);
-        if (e != hipSuccess) return e;
+        if ((e = launch_noise_table(P, st, A)) != hipSuccess) return e;
+        if ((e = launch_fused_k1_blocks(P, st, A)) != hipSuccess) return e;
         if (mid) (void)hipEventRecord(mid, st);
-        const dim3 grd((P.tx1 - P.tx0 + kTaaW - 1) / kTaaW, (P.ty1 - P.ty0 + kTaaH - 1) / kTaaH);
-        if (k1_tone_maps(P))
-            hipLaunchKernelGGL((k_fused_taa<false, float>), grd, dim3(256), 0, st, P, A.tone_out, A.albedo,
-                               A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
-        else if (P.input_half)
-            hipLaunchKernelGGL((k_fused_taa<true, _Float16>), grd, dim3(256), 0, st, P, A.acc_out, A.albedo,
-                               A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
-        else
-            hipLaunchKernelGGL((k_fused_taa<true, float>), grd, dim3(256), 0, st, P, A.acc_out, A.albedo,
-                               A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
-        return hipGetLastError();
+        return launch_fused_k2(P, st, A);
     }
     if (P.not_scaled == 4 && P.scaled == 6) e = launch_fused_t<4, 6>(P, st, A);
     else if (P.not_scaled == 4 && P.scaled == 9) e = launch_fused_t<4, 9>(P, st, A);

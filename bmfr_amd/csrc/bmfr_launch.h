@@ -50,6 +50,12 @@ hipError_t launch_accumulate_filtered(const Params& P, hipStream_t st, const flo
                                       const float* albedo, float* tone, const uint8_t* spp,
                                       const float* acc_prev, float* acc, int frame);
 hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& A, hipEvent_t mid = nullptr);
+// The parts of launch_fused_frame (canonical feature lists): the frame's
+// noise table, K1 over the block rectangle of P (bx0, by0, nbx, nby; empty:
+// nothing), K2 over P's output tile.
+hipError_t launch_noise_table(const Params& P, hipStream_t st, const FusedArgs& A);
+hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedArgs& A);
+hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A);
 hipError_t launch_taa(const Params& P, hipStream_t st, const float2* prev_pixel, const float* new_frame,
                       float* result, const float* prev_frame, int frame);
 

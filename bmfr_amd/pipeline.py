@@ -195,19 +195,38 @@ class Denoiser(_Context):
         super().__init__(cfg, device)
         self.prev_inputs = None
 
-    def process_frame(self, noisy, normals, positions, albedo, prev_vp, jitter, frame: int,
-                      prev_normals=None, prev_positions=None, stream=None) -> None:
-        """Run one frame.  prev_normals / prev_positions default to the ones
-        passed on the previous call (the reference's Double_buffer halves)."""
+    def _call(self, fn: str, noisy, normals, positions, albedo, prev_vp, jitter, frame, prev_normals,
+              prev_positions, stream, done: bool) -> None:
         if frame > 0 and prev_normals is None:
             if self.prev_inputs is None:
                 raise ValueError("frame > 0 needs the previous frame's normals/positions")
             prev_normals, prev_positions = self.prev_inputs
         fi = _lib.FrameInputs(_ptr(noisy), _ptr(normals), _ptr(positions), _ptr(albedo),
                               _ptr(prev_normals), _ptr(prev_positions))
-        check(self.lib.bmfr_process_frame(self.handle, _stream(stream), C.byref(fi), floats(prev_vp, 16),
-                                          floats(jitter, 2), frame), "bmfr_process_frame")
-        self.prev_inputs = (normals, positions)
+        check(getattr(self.lib, fn)(self.handle, _stream(stream), C.byref(fi), floats(prev_vp, 16),
+                                    floats(jitter, 2), frame), fn)
+        if done:
+            self.prev_inputs = (normals, positions)
+
+    def process_frame(self, noisy, normals, positions, albedo, prev_vp, jitter, frame: int,
+                      prev_normals=None, prev_positions=None, stream=None) -> None:
+        """Run one frame.  prev_normals / prev_positions default to the ones
+        passed on the previous call (the reference's Double_buffer halves)."""
+        self._call("bmfr_process_frame", noisy, normals, positions, albedo, prev_vp, jitter, frame,
+                   prev_normals, prev_positions, stream, True)
+
+    def process_frame_interior(self, noisy, normals, positions, albedo, prev_vp, jitter, frame: int,
+                               prev_normals=None, prev_positions=None, stream=None) -> None:
+        """First half of a frame (include/bmfr.h): the K1 blocks that need no
+        halo; may run while the halo exchange of the previous state is in flight."""
+        self._call("bmfr_process_frame_interior", noisy, normals, positions, albedo, prev_vp, jitter, frame,
+                   prev_normals, prev_positions, stream, False)
+
+    def process_frame_border(self, noisy, normals, positions, albedo, prev_vp, jitter, frame: int,
+                             prev_normals=None, prev_positions=None, stream=None) -> None:
+        """Second half: the remaining K1 blocks and K2, once the halo is refreshed."""
+        self._call("bmfr_process_frame_border", noisy, normals, positions, albedo, prev_vp, jitter, frame,
+                   prev_normals, prev_positions, stream, True)
 
     def set_profiling(self, enable: bool, capacity: int = 4096) -> None:
         check(self.lib.bmfr_set_profiling(self.handle, int(enable), capacity), "bmfr_set_profiling")

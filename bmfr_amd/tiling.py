@@ -129,6 +129,13 @@ class HipCopier:
         if err != 0:
             raise RuntimeError(f"hipMemcpy2DAsync failed: {err}")
 
+    def fill2d(self, dst: int, pitch: int, value: int, width: int, rows: int) -> None:
+        self.hip.hipMemset2DAsync.restype = C.c_int
+        self.hip.hipMemset2DAsync.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_size_t, C.c_size_t, C.c_void_p]
+        err = self.hip.hipMemset2DAsync(dst, pitch, value, width, rows, self.stream)
+        if err != 0:
+            raise RuntimeError(f"hipMemset2DAsync failed: {err}")
+
 
 class HostCopier:
     """The same on host memory (CPU tests)."""
@@ -229,6 +236,14 @@ class LoopbackTransport:
                 for src, dst in zip(planes_by_rank[peer], planes_by_rank[rank]):
                     w = r[2] * src.bpp
                     copier.copy2d(dst.rect_ptr(r), dst.pitch, src.rect_ptr(r), src.pitch, w, r[3])
+
+
+def halo_rects(region: Rect, tile: Rect) -> list:
+    """The region minus the tile as up to four rectangles."""
+    rx, ry, rw, rh = region
+    x, y, w, h = tile
+    out = [(rx, ry, rw, y - ry), (rx, y + h, rw, ry + rh - y - h), (rx, y, x - rx, h), (x + w, y, rx + rw - x - w, h)]
+    return [r for r in out if r[2] > 0 and r[3] > 0]
 
 
 def state_planes(denoiser) -> list:

@@ -192,6 +192,21 @@ typedef struct bmfr_frame_inputs {  /* float3 planes, or half3 with input_half *
 bmfr_status bmfr_process_frame(bmfr_ctx *ctx, void *stream, const bmfr_frame_inputs *in,
     const float prev_frame_camera_matrix[16], const float pixel_offset[2], int frame_number);
 
+/* bmfr_process_frame in two calls, to overlap a tiled context's halo
+ * exchange with compute.  _interior (noise table + the K1
+ * blocks whose reads of the previous frame's state stay inside the tile, so
+ * they need no halo) may be issued BEFORE the caller refreshes the halo ring
+ * of bmfr_state(previous = 0) -- which still names the previous frame's
+ * state until _border returns -- and runs while the exchange is in flight;
+ * _border (same arguments, after the refresh is ordered before it on
+ * `stream`) launches the remaining blocks and K2 and completes the frame.
+ * The pair equals bmfr_process_frame bit for bit.  Untiled contexts: every
+ * block is interior. */
+bmfr_status bmfr_process_frame_interior(bmfr_ctx *ctx, void *stream, const bmfr_frame_inputs *in,
+    const float prev_frame_camera_matrix[16], const float pixel_offset[2], int frame_number);
+bmfr_status bmfr_process_frame_border(bmfr_ctx *ctx, void *stream, const bmfr_frame_inputs *in,
+    const float prev_frame_camera_matrix[16], const float pixel_offset[2], int frame_number);
+
 /* Device pointer to the last processed frame's output (TAA result, float3,
  * W*H, the buffer the reference reads back at bmfr.cpp:479-480).  Valid until
  * the next bmfr_process_frame. */

@@ -133,3 +133,25 @@ def test_synth_frame_properties():
     again = bmfr_amd.synth_frame_host(96, 64, 0, clean=True)
     for k in fr:
         assert fr[k].tobytes() == again[k].tobytes()
+
+
+def test_config_struct_matches_header():
+    """The ctypes mirror of bmfr_config has the header's size (input_half is the last field)."""
+    import subprocess
+    import tempfile
+    src = '#include <stdio.h>\n#include "bmfr.h"\nint main(void){printf("%zu %zu", sizeof(bmfr_config), ' \
+          'sizeof(bmfr_frame_inputs));return 0;}\n'
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        cfg_size, in_size = map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split())
+    assert cfg_size == C.sizeof(_lib.Config)
+    assert in_size == C.sizeof(_lib.FrameInputs)
+
+
+def test_split_frame_calls_validate_arguments():
+    lib = _lib.load()
+    assert lib.bmfr_process_frame_interior(None, None, None, None, None, 0) == 1
+    assert lib.bmfr_process_frame_border(None, None, None, None, None, 0) == 1

@@ -12,7 +12,7 @@ import pytest
 import torch
 
 import bmfr_amd
-from bmfr_amd.tiling import HipCopier, LoopbackTransport, TileGrid, state_planes
+from bmfr_amd.tiling import HipCopier, LoopbackTransport, TileGrid, halo_rects, state_planes
 
 pytestmark = pytest.mark.gpu
 
@@ -28,8 +28,12 @@ def _tile_of(a: np.ndarray, region, tile, ch):
 
 @pytest.mark.parametrize("shape", [(320, 256, 2, 2, 40), (352, 224, 2, 1, 48), (256, 320, 1, 2, 40),
                                    (480, 288, 4, 2, 38)])
-@pytest.mark.parametrize("half", [1, 0])
-def test_tiled_matches_untiled_bitwise(shape, half, gpu):
+@pytest.mark.parametrize("half,split", [(1, False), (0, False), (1, True)])
+def test_tiled_matches_untiled_bitwise(shape, half, split, gpu):
+    """split: each frame as bmfr_process_frame_interior, halo exchange,
+    bmfr_process_frame_border -- with the halo ring poisoned (all-ones bytes:
+    NaN colours, spp 255) until the exchange, so an interior block that read
+    the halo would break the bitwise match."""
     W, H, tx, ty, halo = shape
     grid = TileGrid(W, H, tx, ty, halo=halo)
     full = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H,
@@ -47,14 +51,32 @@ def test_tiled_matches_untiled_bitwise(shape, half, gpu):
         _, jit = bmfr_amd.synth_camera(W, H, f)
         fr = bmfr_amd.synth_frame_device(W, H, f)
         full.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, f)
-        if f > 0:
-            loop.exchange_all([state_planes(d) for d in tiles], copier)
-        for r, d in enumerate(tiles):
-            inp = bmfr_amd.synth_region_device(W, H, d.region, f)
-            d.process_frame(inp["noisy"], inp["normals"], inp["positions"], inp["albedo"], vp, jit, f,
-                            prev_normals=prev[r]["normals"] if prev[r] else None,
-                            prev_positions=prev[r]["positions"] if prev[r] else None)
-            prev[r] = inp
+        inps = [bmfr_amd.synth_region_device(W, H, d.region, f) for d in tiles]
+
+        def call(method, r):
+            inp = inps[r]
+            getattr(tiles[r], method)(inp["noisy"], inp["normals"], inp["positions"], inp["albedo"], vp, jit, f,
+                                      prev_normals=prev[r]["normals"] if prev[r] else None,
+                                      prev_positions=prev[r]["positions"] if prev[r] else None)
+
+        if split:
+            if f > 0:
+                for r, d in enumerate(tiles):
+                    for p in state_planes(d):
+                        for h in halo_rects(d.region, grid.tile(r)):
+                            copier.fill2d(p.rect_ptr(h), p.pitch, 0xFF, h[2] * p.bpp, h[3])
+            for r in range(grid.ranks):
+                call("process_frame_interior", r)
+            if f > 0:
+                loop.exchange_all([state_planes(d) for d in tiles], copier)
+            for r in range(grid.ranks):
+                call("process_frame_border", r)
+        else:
+            if f > 0:
+                loop.exchange_all([state_planes(d) for d in tiles], copier)
+            for r in range(grid.ranks):
+                call("process_frame", r)
+        prev = inps
         torch.cuda.synchronize()
         n = W * H
         want = {

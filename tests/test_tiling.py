@@ -104,3 +104,16 @@ def test_halo_exchange_gloo(shape):
     for rank, ok, sent in res:
         assert ok is True, (rank, ok)
         assert sent > 0
+
+
+@pytest.mark.parametrize("region,tile", [((0, 0, 100, 80), (20, 10, 50, 40)), ((0, 0, 100, 80), (0, 0, 60, 80)),
+                                         ((10, 20, 70, 50), (10, 20, 70, 50))])
+def test_halo_rects_partition_region_minus_tile(region, tile):
+    from bmfr_amd.tiling import halo_rects
+    m = np.zeros((200, 200), np.int32)
+    for x, y, w, h in halo_rects(region, tile):
+        m[y:y + h, x:x + w] += 1
+    x, y, w, h = tile
+    m[y:y + h, x:x + w] += 1
+    rx, ry, rw, rh = region
+    assert (m[ry:ry + rh, rx:rx + rw] == 1).all() and m.sum() == rw * rh
