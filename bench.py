@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="multi-GPU: weak = one --width x --height tile per GPU, strong = one frame split")
     ap.add_argument("--halo", type=int, default=64, help="tile halo in pixels (>= 34 + max motion)")
+    ap.add_argument("--sequence", action="store_true",
+                    help="single GPU: the timed frames as one bmfr_process_sequence call (TAA of frame f beside "
+                         "K1 of frame f+1) instead of one bmfr_process_frame per frame")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="multi-GPU: exchange the halo before the frame instead of under K1's interior blocks")
     return ap.parse_args()
@@ -125,7 +128,7 @@ def pmc_traffic(workload: str):
     return d.get(workload, {}).get("hbm_bytes_per_launch")
 
 
-def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup):
+def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, per_frame=False):
     """Denoise frames 0..warmup+steps-1 of the synthetic W x H sequence (this
     rank's tile of it); time the last `steps` frames.  Returns the timings,
     per-kernel HIP-event means and the PSNR of the last output."""
@@ -181,16 +184,26 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup):
         if frame_done is not None:
             frame_done.record(compute)
 
-    for f in range(warmup):
-        run(f)
+    # Untiled: the whole run as bmfr_process_sequence calls (frames pipelined),
+    # unless per_frame; tiled: frame by frame around the halo exchange.
+    pipelined = grid is None and not per_frame
+
+    def run_range(f0, f1):
+        if pipelined:
+            den.process_sequence(frames[f0:f1], cams[f0:f1], f0)
+        else:
+            for f in range(f0, f1):
+                run(f)
+
+    if warmup:
+        run_range(0, warmup)
     torch.cuda.synchronize()
     den.set_profiling(True, capacity=max(steps, 1))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for f in range(warmup, nfr):
-        run(f)
+    run_range(warmup, nfr)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -246,12 +259,13 @@ def main():
         W, H = a.width, a.height
     grid = tiling.TileGrid(W, H, tx, ty, halo=a.halo) if world > 1 else None
     tile = grid.tile(rank) if grid else (0, 0, W, H)
-    r = run_sequence(a, W, H, tile, grid, rank, world, dev, backend, a.steps, a.warmup)
+    r = run_sequence(a, W, H, tile, grid, rank, world, dev, backend, a.steps, a.warmup, per_frame=not a.sequence)
     cfg = r["cfg"]
     # The metric's second resolution (BASELINE.json: ms/frame @1080p & 4K), single GPU only.
     r1080 = None
     if world == 1 and not a.no_1080p and (W, H) != (1920, 1080):
-        r1080 = run_sequence(a, 1920, 1080, (0, 0, 1920, 1080), None, 0, 1, dev, backend, a.steps, a.warmup)
+        r1080 = run_sequence(a, 1920, 1080, (0, 0, 1920, 1080), None, 0, 1, dev, backend, a.steps, a.warmup,
+                             per_frame=not a.sequence)
 
     s = 2 if a.input_half else 4
     tile_px = tile[2] * tile[3]
@@ -275,6 +289,7 @@ def main():
             "data": "synthetic (GPU-rendered 1-spp frames + features, resident in HBM)",
             "config": {"workload": workload, "image": f"{W}x{H}", "buffer_count": cfg.buffer_count,
                        "half_tmp_data": a.half_tmp, "input_half": int(a.input_half), "frames_timed": a.steps,
+                       "frames_pipelined": world == 1 and a.sequence,
                        "parallelism": (f"tiles {tx}x{ty}, halo {a.halo} px, "
                                        f"{'RCCL' if backend == 'nccl' else backend} halo exchange"
                                        f"{' overlapped with interior blocks' if a.overlap else ''}")

@@ -27,7 +27,11 @@ struct bmfr_ctx {
     float* acc[2] = {nullptr, nullptr};
     float* result[2] = {nullptr, nullptr};
     float* tone = nullptr;
-    float2* prev_pixel = nullptr;
+    float2* prev_pixel[2] = {nullptr, nullptr};  // double-buffered: K2 of frame f reads it while K1 of f+1 writes
+    // bmfr_process_sequence: side stream for K2 and a ring of ordering events
+    hipStream_t side = nullptr;
+    static constexpr int kSeqEvents = 4;
+    hipEvent_t seq_k1[kSeqEvents] = {}, seq_k2[kSeqEvents] = {}, seq_start = nullptr;
     double* noise_table = nullptr;
     unsigned long long* stamps = nullptr;  // diagnostic: BMFR_STAMPS=1 with libbmfr_diag.so
     int cur = 0;
@@ -282,7 +286,7 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
         if (e == hipSuccess) e = hipMalloc(&c->result[i], px * 3 * sizeof(float));
     }
     if (e == hipSuccess) e = hipMalloc(&c->tone, px * 3 * sizeof(float));
-    if (e == hipSuccess) e = hipMalloc(&c->prev_pixel, px * sizeof(float2));
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipMalloc(&c->prev_pixel[i], px * sizeof(float2));
     if (e == hipSuccess && std::getenv("BMFR_STAMPS"))
         e = hipMalloc(&c->stamps, (size_t)sz.blocks * 8 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&c->noise_table, (size_t)bmfr::kMaxFeatures * bmfr::kBlockPixels * sizeof(double));
@@ -307,7 +311,15 @@ bmfr_status bmfr_destroy(bmfr_ctx* c) {
     delete[] c->prof_events;
     delete[] c->prof_frames;
     (void)hipFree(c->tone);
-    (void)hipFree(c->prev_pixel);
+    for (int i = 0; i < 2; ++i) (void)hipFree(c->prev_pixel[i]);
+    if (c->side) {
+        (void)hipStreamDestroy(c->side);
+        for (int i = 0; i < bmfr_ctx::kSeqEvents; ++i) {
+            (void)hipEventDestroy(c->seq_k1[i]);
+            (void)hipEventDestroy(c->seq_k2[i]);
+        }
+        (void)hipEventDestroy(c->seq_start);
+    }
     (void)hipFree(c->noise_table);
     (void)hipFree(c->stamps);
     delete c;
@@ -422,7 +434,7 @@ bmfr::FusedArgs frame_args(const bmfr_ctx* c, const bmfr_frame_inputs* in, const
     A.result_prev = c->result[prv];
     A.noisy_out = c->noisy_acc[cur];
     A.spp_out = c->spp[cur];
-    A.prev_pixel_out = c->prev_pixel;
+    A.prev_pixel_out = c->prev_pixel[cur];
     A.acc_out = c->acc[cur];
     A.tone_out = c->tone;
     A.result_out = c->result[cur];
@@ -537,6 +549,84 @@ bmfr_status bmfr_process_frame(bmfr_ctx* c, void* stream, const bmfr_frame_input
     return process_part(c, stream, in, prev_frame_camera_matrix, pixel_offset, frame_number, 2);
 }
 
+bmfr_status bmfr_process_sequence(bmfr_ctx* c, void* stream, int count, const bmfr_frame_inputs* in,
+                                  const float* prev_frame_camera_matrices, const float* pixel_offsets,
+                                  int first_frame, float* const* outputs) {
+    if (!c || count <= 0 || !in || !prev_frame_camera_matrices || !pixel_offsets || first_frame < 0)
+        return BMFR_ERROR_INVALID_ARGUMENT;
+    if (c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // tiles exchange a halo between frames
+    const hipStream_t s = as_stream(stream);
+    const size_t out_bytes = c->sizes.region_bytes;
+    const bool pipelined = bmfr::fused_supported(c->P) && !bmfr::k1_tone_maps(c->P);
+    bmfr_status st;
+    if (!pipelined) {  // frame after frame on `stream`
+        for (int i = 0; i < count; ++i) {
+            st = bmfr_process_frame(c, stream, &in[i], prev_frame_camera_matrices + 16 * i, pixel_offsets + 2 * i,
+                                    first_frame + i);
+            if (st != BMFR_OK) return st;
+            if (outputs && outputs[i])
+                if ((st = hip_status(hipMemcpyAsync(outputs[i], c->result[c->cur], out_bytes, hipMemcpyDefault, s))))
+                    return st;
+        }
+        return BMFR_OK;
+    }
+    if (first_frame > 0 && !c->has_frame) return BMFR_ERROR_INVALID_ARGUMENT;
+    for (int i = 0; i < count; ++i) {
+        const bmfr_frame_inputs& x = in[i];
+        if (!x.noisy || !x.normals || !x.positions || !x.albedo) return BMFR_ERROR_INVALID_ARGUMENT;
+        if (first_frame + i > 0 && (!x.prev_normals || !x.prev_positions)) return BMFR_ERROR_INVALID_ARGUMENT;
+    }
+    hipError_t e = hipSuccess;
+    if (!c->side) {
+        e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+        for (int i = 0; i < bmfr_ctx::kSeqEvents && e == hipSuccess; ++i) {
+            e = hipEventCreateWithFlags(&c->seq_k1[i], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&c->seq_k2[i], hipEventDisableTiming);
+        }
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->seq_start, hipEventDisableTiming);
+        if (e != hipSuccess) return hip_status(e);
+    }
+    // K1 of frame f on `stream`, K2 of frame f on the side stream, so that K2
+    // of frame f runs beside K1 of frame f+1.  K1 of f waits for K2 of f-2,
+    // the last reader of the state slot (accumulated filtered colour,
+    // prev-frame pixel) it overwrites; the call joins `stream` at the end.
+    const hipStream_t t = c->side;
+    (void)hipEventRecord(c->seq_start, s);
+    (void)hipStreamWaitEvent(t, c->seq_start, 0);
+    for (int i = 0; i < count; ++i) {
+        const int f = first_frame + i;
+        const int cur = c->has_frame ? 1 - c->cur : 0;
+        const bmfr::FusedArgs A = frame_args(c, &in[i], prev_frame_camera_matrices + 16 * i, pixel_offsets + 2 * i,
+                                             f, cur);
+        const Params P = frame_params(c, f);
+        hipEvent_t* ev = nullptr;
+        if (c->prof_capacity > 0) {
+            const int slot = (int)(c->prof_count % c->prof_capacity);
+            ev = c->prof_events + 3 * slot;
+            c->prof_frames[slot] = f;
+            ++c->prof_count;
+        }
+        const int k = i % bmfr_ctx::kSeqEvents;
+        if (i >= 2) e = hipStreamWaitEvent(s, c->seq_k2[(i - 2) % bmfr_ctx::kSeqEvents], 0);
+        if (ev && e == hipSuccess) e = hipEventRecord(ev[0], s);
+        if (e == hipSuccess) e = bmfr::launch_noise_table(P, s, A);
+        if (e == hipSuccess) e = bmfr::launch_fused_k1_blocks(P, s, A);
+        if (ev && e == hipSuccess) e = hipEventRecord(ev[1], s);
+        if (e == hipSuccess) e = hipEventRecord(c->seq_k1[k], s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(t, c->seq_k1[k], 0);
+        if (e == hipSuccess) e = bmfr::launch_fused_k2(P, t, A);
+        if (e == hipSuccess && outputs && outputs[i])
+            e = hipMemcpyAsync(outputs[i], A.result_out, out_bytes, hipMemcpyDefault, t);
+        if (ev && e == hipSuccess) e = hipEventRecord(ev[2], t);
+        if (e == hipSuccess) e = hipEventRecord(c->seq_k2[k], t);
+        if (e != hipSuccess) return hip_status(e);
+        c->cur = cur;
+        c->has_frame = true;
+    }
+    return hip_status(hipStreamWaitEvent(s, c->seq_k2[(count - 1) % bmfr_ctx::kSeqEvents], 0));
+}
+
 bmfr_status bmfr_process_frame_interior(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
                                         const float prev_frame_camera_matrix[16], const float pixel_offset[2],
                                         int frame_number) {
@@ -615,7 +705,7 @@ bmfr_status bmfr_state(const bmfr_ctx* c, int previous, bmfr_state_view* out) {
     out->spp = c->spp[i];
     out->filtered_accumulated = c->acc[i];
     out->tone_mapped = c->tone;
-    out->prev_frame_pixel = reinterpret_cast<float*>(c->prev_pixel);
+    out->prev_frame_pixel = reinterpret_cast<float*>(c->prev_pixel[i]);
     out->accept = nullptr;  // the fused kernel keeps accept bits in registers
     out->result = c->result[i];
     return BMFR_OK;

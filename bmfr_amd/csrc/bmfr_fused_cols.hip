@@ -36,34 +36,36 @@ constexpr int kThreads = 256;
 constexpr int kSlots = 16;    // rows per lane per column (row = lane + 64 j)
 constexpr int kUStride = 20;  // floats per lane in a u buffer: 16 + 4 (conflict-free 16-byte reads)
 
+#ifndef BMFR_PARK_GLOBAL
+// Phase 1 -> 3 hand-over of the previous accumulated filtered colour
+// (bmfr.cl:786-842, read at the noisy accumulation's taps): 0 = parked in
+// LDS (12 KB per block); 1 = parked in the owner pixel of the output plane
+// acc_out itself, which phase 3 then overwrites (same thread, same address:
+// program order) -- no LDS, so 5 blocks/CU fit, but measured slower
+// (0.446 vs 0.434 ms at 4K, and 0.465 at 5 blocks/CU with the spills that
+// 96 VGPRs cost).
+#define BMFR_PARK_GLOBAL 0
+#endif
+
 template <int B>
 struct Lds {
-#ifdef BMFR_KEEP_ALIAS
-    // phase 1 -> 3: previous accumulated filtered colour per item, held in
-    // registers through phase 1 and parked in the matrix area once it is free
-    static constexpr bool kKeepAlias = true;
-    union {
-        _Float16 M[B - 1][64 * kSlots];  // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
-        struct {
-            float u[2][64 * kUStride];    // Householder vectors, double-buffered by column parity
-            float keep[4][3][kThreads];
-        };
-    };
-#else
-    static constexpr bool kKeepAlias = false;
     union {
         _Float16 M[B - 1][64 * kSlots];  // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
         float u[2][64 * kUStride];       // Householder vectors, double-buffered by column parity
     };
+#if !BMFR_PARK_GLOBAL
     float keep[4][3][kThreads];  // phase 1 -> 3: previous accumulated filtered colour per item
 #endif
     float piv[2][2];                    // |u|^2 and RN(1/|u|^2) of the published vector
     float R[(B - 2) * (B - 2) * 3];     // R[x][y][ch], x = column (as k_fused)
     float weights[(B - 3) * 3];
     float mm[3 * (B - 3)];              // per scaled feature: min, max, 1/(max-min)
+#ifdef BMFR_LDS_PAD
+    float pad[BMFR_LDS_PAD / 4];        // occupancy experiments only
+#endif
 };
-static_assert(sizeof(float) * (2 * 64 * kUStride + 4 * 3 * kThreads) <= sizeof(_Float16) * 12 * 64 * kSlots,
-              "u buffers and parked colours must fit in the matrix area (B >= 13)");
+static_assert(sizeof(float) * 2 * 64 * kUStride <= sizeof(_Float16) * 12 * 64 * kSlots,
+              "u buffers must fit in the matrix area (B >= 13)");
 
 template <int... I, class F>
 __device__ __forceinline__ void sfor_impl(std::integer_sequence<int, I...>, F&& f) {
@@ -243,6 +245,23 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B>& L, int l
     }
 }
 
+#ifndef BMFR_LDS_BARRIERS
+#define BMFR_LDS_BARRIERS 1
+#endif
+// The work-group shares data through LDS only, so its barriers need not
+// wait for its global loads and stores (__syncthreads() does).
+__device__ __forceinline__ void k1_barrier() {
+    if constexpr (BMFR_LDS_BARRIERS) lds_barrier();
+    else __syncthreads();
+}
+
+#ifndef BMFR_P3_EARLY
+#define BMFR_P3_EARLY 1  // phase-3 loads in flight across back substitution
+#endif
+#ifndef BMFR_PIVOT_PRIO
+#define BMFR_PIVOT_PRIO 0  // s_setprio while a wave computes and publishes the next pivot column
+#endif
+
 // Wave W's part of the fit: columns c = W (mod 4), c >= 1 (column 0 is implicit).
 template <int W, int NS, int FS>
 struct WaveFit {
@@ -285,8 +304,11 @@ struct WaveFit {
                 }
                 const float ulen2 = L.piv[c & 1][0], recip = L.piv[c & 1][1];
                 if constexpr (publish) {
+                    // the next pivot is every wave's critical path: issue it first
+                    if (BMFR_PIVOT_PRIO) __builtin_amdgcn_s_setprio(BMFR_PIVOT_PRIO);
                     update_column<c>(a[nxt >> 2], u, ulen2, recip, l);
                     publish_pivot<nxt, B>(a[nxt >> 2], L, l);
+                    if (BMFR_PIVOT_PRIO) __builtin_amdgcn_s_setprio(0);
                 }
                 sfor<NSL>([&](auto K) {
                     constexpr int fb = W + 4 * decltype(K)::value;
@@ -295,7 +317,7 @@ struct WaveFit {
                 });
             }
         }
-        if constexpr (c + 1 < NF) __syncthreads();  // u_{c+1} published
+        if constexpr (c + 1 < NF) k1_barrier();  // u_{c+1} published
     }
 
     template <int... C>
@@ -319,7 +341,7 @@ struct WaveFit {
                 for (int i = 0; i < 8; ++i) a[c >> 2][i] = __builtin_bit_cast(h2, w[i]);
             }
         });
-        __syncthreads();  // the u buffers alias M
+        k1_barrier();  // the u buffers alias M
         after_load();
 
         // Scale the position features to the block's [min, max] (bmfr.cl:510-542).
@@ -434,8 +456,7 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
     uint32_t spps = 0;   // per item i, bits 8i..8i+7: its new spp
     uint32_t ibits = 0;  // per item i, bit i: owner; bit 4 + i: accepted taps with weight > 0
     // The temporal part of accumulate_filtered_data is read at the noisy
-    // accumulation's taps (bmfr.cl:786-842) and parked in LDS for phase 3.
-    f3 keep_prev[4];
+    // accumulation's taps (bmfr.cl:786-842) and parked for phase 3.
 #ifndef BMFR_P1_BATCH
 #define BMFR_P1_BATCH 2  // items whose current-frame loads are issued together (4: > 128 VGPRs)
 #endif
@@ -465,13 +486,13 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
             }
             spps |= (uint32_t)it.spp << (8 * i);
             ibits |= ((uint32_t)it.owner << i) | ((uint32_t)it.prev_f_divided << (4 + i));
-            if constexpr (Lds<B>::kKeepAlias) {
-                keep_prev[i] = it.prev_f;
-            } else {
-                L.keep[i][0][t] = it.prev_f.x;  // parked for phase 3
-                L.keep[i][1][t] = it.prev_f.y;
-                L.keep[i][2][t] = it.prev_f.z;
-            }
+#if BMFR_PARK_GLOBAL
+            if (it.owner) st3(acc_out, it.lin, it.prev_f);
+#else
+            L.keep[i][0][t] = it.prev_f.x;
+            L.keep[i][1][t] = it.prev_f.y;
+            L.keep[i][2][t] = it.prev_f.z;
+#endif
             if (it.owner) {
                 st3(noisy_out, it.lin, it.color);
                 spp_out[it.lin] = it.spp;
@@ -490,34 +511,20 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 #endif
         }
     }
-    __syncthreads();
+    k1_barrier();  // matrix in LDS; phase 1's global stores drain in the background
     BMFR_STAMP(1);
     BMFR_STAMP(2);  // scaling runs inside the per-wave fit
 
     // ---- fit: min/max scaling, Householder QR, right-hand side ----
-    const auto park = [&] {
-        if constexpr (Lds<B>::kKeepAlias) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                L.keep[i][0][t] = keep_prev[i].x;
-                L.keep[i][1][t] = keep_prev[i].y;
-                L.keep[i][2][t] = keep_prev[i].z;
-            }
-        }
-    };
+    const auto park = [] {};
     switch (w) {
         case 0: WaveFit<0, NS, FS>::run(L, l, noise, P.noise2, park); break;
         case 1: WaveFit<1, NS, FS>::run(L, l, noise, P.noise2, park); break;
         case 2: WaveFit<2, NS, FS>::run(L, l, noise, P.noise2, park); break;
         default: WaveFit<3, NS, FS>::run(L, l, noise, P.noise2, park); break;
     }
-    __syncthreads();
-    BMFR_STAMP(3);
-    back_substitute<B>(L, t);
-    __syncthreads();
-    BMFR_STAMP(4);
-
-    // ---- weighted_sum (bmfr.cl:717-750) + temporal blend (bmfr.cl:778-849) ----
+    // Phase 3's loads (normal and position of the four items, bmfr.cl:725-729)
+    // go out now: they land while wave 0 back-substitutes and the others wait.
     int l3 = l;  // opaque copy: recompute phase-1 addresses instead of keeping them live across the fit
     asm volatile("" : "+v"(l3));
     const int2 off = kBlockOffsets[frame & 15];
@@ -531,34 +538,72 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
         nrm[i] = ld3in<IN>(in.n_cur, lin[i]);
         wp[i] = ld3in<IN>(in.p_cur, lin[i]);
     }
+#if BMFR_P3_EARLY
+    k1_barrier();  // R complete (LDS); with LDS-only barriers the loads above stay in flight
+    BMFR_STAMP(3);
+    back_substitute<B>(L, t);
+    k1_barrier();  // weights complete
+#else
+    __syncthreads();
+    BMFR_STAMP(3);
+    back_substitute<B>(L, t);
+    __syncthreads();
+#endif
+    BMFR_STAMP(4);
+
+    // ---- weighted_sum (bmfr.cl:717-750) + temporal blend (bmfr.cl:778-849) ----
+#if BMFR_PARK_GLOBAL
+    f3 parked[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (ibits & (1u << i)) parked[i] = ld3(acc_out, lin[i]);  // this thread's phase-1 store
+#endif
+    // Features outer, items inner: each weight / min-max is live for one
+    // feature only.  Every item still accumulates in feature order.
+    f3 c[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[i] = f3{0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < B - 3; ++f) {
+        const float w0 = L.weights[3 * f], w1 = L.weights[3 * f + 1], w2 = L.weights[3 * f + 2];
+        float bmin = 0.f, d = 0.f, rcp = 0.f;
+        if (f >= NS) {
+            bmin = L.mm[3 * (f - NS)];
+            d = L.mm[3 * (f - NS) + 1] - bmin;
+            rcp = L.mm[3 * (f - NS) + 2];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float v = feature_value(f, nrm[i], wp[i]);
+            if (f >= NS) {
+                v = v - bmin;
+                if (fabsf(d) > 1.0f) v = div_by_recip(v, d, rcp);
+            }
+            c[i].x = c[i].x + w0 * v;
+            c[i].y = c[i].y + w1 * v;
+            c[i].z = c[i].z + w2 * v;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one feature's weights live at a time
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (ibits & (1u << i)) {
-            f3 c{0.f, 0.f, 0.f};
-#pragma unroll
-            for (int f = 0; f < B - 3; ++f) {
-                float v = feature_value(f, nrm[i], wp[i]);
-                if (f >= NS) {
-                    const float bmin = L.mm[3 * (f - NS)], bmax = L.mm[3 * (f - NS) + 1];
-                    const float d = bmax - bmin;
-                    v = v - bmin;
-                    if (fabsf(d) > 1.0f) v = div_by_recip(v, d, L.mm[3 * (f - NS) + 2]);
-                }
-                c.x = c.x + L.weights[3 * f] * v;
-                c.y = c.y + L.weights[3 * f + 1] * v;
-                c.z = c.z + L.weights[3 * f + 2] * v;
-            }
-            c.x = c.x < 0.f ? 0.f : c.x;
-            c.y = c.y < 0.f ? 0.f : c.y;
-            c.z = c.z < 0.f ? 0.f : c.z;
+            f3 ci = c[i];
+            ci.x = ci.x < 0.f ? 0.f : ci.x;
+            ci.y = ci.y < 0.f ? 0.f : ci.y;
+            ci.z = ci.z < 0.f ? 0.f : ci.z;
             // bmfr.cl:834-849: alpha from the current spp when the taps carried weight
             const float alpha = (ibits & (1u << (4 + i)))
                                     ? fmaxf(1.f / (float)((spps >> (8 * i)) & 255u), P.second_blend_alpha)
                                     : 1.f;
             const float beta = 1.f - alpha;
+#if BMFR_PARK_GLOBAL
+            const f3 prev = parked[i];
+#else
             const int t3 = l3 + 64 * w;
             const f3 prev{L.keep[i][0][t3], L.keep[i][1][t3], L.keep[i][2][t3]};
-            const f3 acc{alpha * c.x + beta * prev.x, alpha * c.y + beta * prev.y, alpha * c.z + beta * prev.z};
+#endif
+            const f3 acc{alpha * ci.x + beta * prev.x, alpha * ci.y + beta * prev.y, alpha * ci.z + beta * prev.z};
             st3(acc_out, lin[i], acc);
         }
     }

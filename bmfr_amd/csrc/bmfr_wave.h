@@ -13,6 +13,13 @@
 
 namespace bmfr {
 
+// Work-group barrier ordering LDS only: __syncthreads() also orders global
+// memory, i.e. waits for every outstanding global load of the wave
+// (vmcnt(0)) -- this one lets loads stay in flight across the barrier.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // lane l <- lane l+8 within its 16-lane row (valid for l % 16 < 8)
 __device__ __forceinline__ float dpp_shl8(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x108, 0xf, 0xf, true));

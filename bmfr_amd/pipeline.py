@@ -215,6 +215,28 @@ class Denoiser(_Context):
         self._call("bmfr_process_frame", noisy, normals, positions, albedo, prev_vp, jitter, frame,
                    prev_normals, prev_positions, stream, True)
 
+    def process_sequence(self, frames, cameras, first_frame: int, outputs=None, stream=None) -> None:
+        """Frames first_frame .. first_frame+len(frames)-1 in one pipelined call
+        (include/bmfr.h bmfr_process_sequence).  frames: dicts with noisy,
+        normals, positions, albedo tensors; cameras: (prev_vp, jitter) per
+        frame; outputs: optional tensors receiving each frame's output."""
+        n = len(frames)
+        arr = (_lib.FrameInputs * n)()
+        prev = self.prev_inputs
+        for i, fr in enumerate(frames):
+            pn, pp = prev if prev is not None else (None, None)
+            arr[i] = _lib.FrameInputs(_ptr(fr["noisy"]), _ptr(fr["normals"]), _ptr(fr["positions"]),
+                                      _ptr(fr["albedo"]), _ptr(pn), _ptr(pp))
+            prev = (fr["normals"], fr["positions"])
+        vps = floats([v for vp, _ in cameras for v in vp], 16 * n)
+        offs = floats([v for _, jit in cameras for v in jit], 2 * n)
+        outs = None
+        if outputs is not None:
+            outs = (C.c_void_p * n)(*[_ptr(o) for o in outputs])
+        check(self.lib.bmfr_process_sequence(self.handle, _stream(stream), n, arr, vps, offs, first_frame, outs),
+              "bmfr_process_sequence")
+        self.prev_inputs = prev
+
     def process_frame_interior(self, noisy, normals, positions, albedo, prev_vp, jitter, frame: int,
                                prev_normals=None, prev_positions=None, stream=None) -> None:
         """First half of a frame (include/bmfr.h): the K1 blocks that need no

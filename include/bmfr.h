@@ -207,6 +207,22 @@ bmfr_status bmfr_process_frame_interior(bmfr_ctx *ctx, void *stream, const bmfr_
 bmfr_status bmfr_process_frame_border(bmfr_ctx *ctx, void *stream, const bmfr_frame_inputs *in,
     const float prev_frame_camera_matrix[16], const float pixel_offset[2], int frame_number);
 
+/* `count` consecutive frames first_frame .. first_frame+count-1 in one call
+ * (the whole loop of bmfr.cpp:417-485 over frames already in device memory,
+ * as tasks() holds the sequence in memory): in[i], the column-major
+ * prev_frame_camera_matrices[16*i..] and pixel_offsets[2*i..] are frame
+ * first_frame+i's arguments of bmfr_process_frame.  The frames are
+ * pipelined: TAA of frame f (K2) runs on a context-owned stream beside K1 of
+ * frame f+1; all work is joined back onto `stream`, so everything the call
+ * enqueues is complete when `stream` reaches the point after it.  All
+ * inputs must stay valid until then.  outputs (nullable; entries nullable):
+ * outputs[i] receives frame i's output (W*H float3, device or page-locked
+ * host memory).  Results equal bmfr_process_frame per frame bit for bit.
+ * Untiled contexts only (tiles exchange a halo between frames). */
+bmfr_status bmfr_process_sequence(bmfr_ctx *ctx, void *stream, int count, const bmfr_frame_inputs *in,
+    const float *prev_frame_camera_matrices, const float *pixel_offsets, int first_frame,
+    float *const *outputs);
+
 /* Device pointer to the last processed frame's output (TAA result, float3,
  * W*H, the buffer the reference reads back at bmfr.cpp:479-480).  Valid until
  * the next bmfr_process_frame. */
