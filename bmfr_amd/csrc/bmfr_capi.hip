@@ -358,7 +358,8 @@ bmfr_status bmfr_accumulate_noisy_data(bmfr_ctx* c, void* stream, float* out_pre
 
 bmfr_status bmfr_fitter(bmfr_ctx* c, void* stream, float* weights, float* mins_maxs, void* tmp_data,
                         int frame_number) {
-    if (!c || !weights || !mins_maxs || !tmp_data || frame_number < 0) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (!c || !weights || (!mins_maxs && c->P.scaled > 0) || !tmp_data || frame_number < 0)
+        return BMFR_ERROR_INVALID_ARGUMENT;
     if (!stage_api_ok(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
     if (!bmfr::fitter_supported(c->P.not_scaled, c->P.scaled)) return BMFR_ERROR_UNSUPPORTED;
     return hip_status(bmfr::launch_fitter(c->P, as_stream(stream), weights, mins_maxs, tmp_data, frame_number));
@@ -369,7 +370,8 @@ bmfr_status bmfr_weighted_sum(bmfr_ctx* c, void* stream, const float* weights, c
                               const float* current_positions, const float* current_noisy,
                               int frame_number) {
     (void)current_noisy;  // debugging-only argument upstream (bmfr.cl:709)
-    if (!c || !weights || !mins_maxs || !output || !current_normals || !current_positions || frame_number < 0)
+    if (!c || !weights || (!mins_maxs && c->P.scaled > 0) || !output || !current_normals || !current_positions ||
+        frame_number < 0)
         return BMFR_ERROR_INVALID_ARGUMENT;
     if (!stage_api_ok(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
     return hip_status(bmfr::launch_weighted_sum(c->P, as_stream(stream), weights, mins_maxs, output,

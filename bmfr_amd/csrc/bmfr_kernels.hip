@@ -10,6 +10,7 @@
 //    (upstream round-trips it through HBM ~30 times per block, bmfr.cl:555-656);
 //    K2 = TAA (needs the 3x3 neighbourhood across block borders).
 #include "bmfr_kernels.h"
+#include "bmfr_generic.h"
 #include "bmfr_launch.h"
 
 namespace bmfr {
@@ -46,54 +47,7 @@ __global__ __launch_bounds__(256) void k_accumulate_noisy(Params P, NoisyInputs 
     }
 }
 
-// ---------------------------------------------------------------- stage 2 --
-template <int NS, int FS, bool HALF>
-__global__ __launch_bounds__(256) void k_fitter(Params P, float* __restrict__ weights,
-                                                float* __restrict__ mins_maxs, void* tmp, int frame) {
-    constexpr int B = NS + FS + 3;
-    __shared__ FitLds<B> L;
-    const int t = threadIdx.x, g = blockIdx.x;
-    const size_t base = (size_t)g * B * kBlockPixels;
-    float a[B][kSubs];
-#pragma unroll
-    for (int f = 0; f < B; ++f)
-#pragma unroll
-        for (int s = 0; s < kSubs; ++s) {
-            const size_t i = base + (size_t)f * kBlockPixels + t + s * kLocal;
-            a[f][s] = HALF ? (float)((const _Float16*)tmp)[i] : ((const float*)tmp)[i];
-        }
-    fit_block<NS, FS, HALF, true, false>(a, L, t, frame, P.noise2);
-#pragma unroll
-    for (int f = 0; f < B; ++f)
-#pragma unroll
-        for (int s = 0; s < kSubs; ++s) {
-            const size_t i = base + (size_t)f * kBlockPixels + t + s * kLocal;
-            if (HALF) ((_Float16*)tmp)[i] = (_Float16)a[f][s];
-            else ((float*)tmp)[i] = a[f][s];
-        }
-    if (t < (B - 3) * 3) weights[(size_t)g * (B - 3) * 3 + t] = L.weights[t];
-    if (t < FS * 2) mins_maxs[(size_t)g * FS * 2 + t] = L.minmax[t];
-}
-
 // ---------------------------------------------------------------- stage 3 --
-// Features recomputed in f32 from normals/positions, scaled with the block's
-// min/max, dotted with the block's weights (bmfr.cl:703-758).
-__device__ __forceinline__ f3 weighted_color(const Params& P, const float* __restrict__ w,
-                                             const float* __restrict__ mm, f3 n, f3 p) {
-    f3 c{0.f, 0.f, 0.f};
-    for (int f = 0; f < P.buffers - 3; ++f) {
-        float v = feature_value(P.codes[f], n, p);
-        if (f >= P.not_scaled) v = scale(v, mm[2 * (f - P.not_scaled)], mm[2 * (f - P.not_scaled) + 1]);
-        c.x = c.x + w[3 * f] * v;
-        c.y = c.y + w[3 * f + 1] * v;
-        c.z = c.z + w[3 * f + 2] * v;
-    }
-    c.x = c.x < 0.f ? 0.f : c.x;
-    c.y = c.y < 0.f ? 0.f : c.y;
-    c.z = c.z < 0.f ? 0.f : c.z;
-    return c;
-}
-
 __device__ __forceinline__ int block_of_pixel(const Params& P, int x, int y, int frame) {
     const int2 off = kBlockOffsets[frame & 15];
     return (x + kEdge / 2 - off.x) / kEdge + ((y + kEdge / 2 - off.y) / kEdge) * P.blocks_x;
@@ -246,68 +200,6 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
     }
 }
 
-// ------------------------------------------- generic-feature fused K1 ----
-// Fallback K1 for feature lists other than the canonical ones (runtime
-// feature codes); the canonical lists use k_fused (bmfr_fused.hip).
-template <int NS, int FS, bool HALF>
-__global__ __launch_bounds__(256) void k_fused_block(Params P, NoisyInputs in, Camera cam, int frame,
-                                                     const float* __restrict__ albedo,
-                                                     const float* __restrict__ acc_prev,
-                                                     float* __restrict__ noisy_out,
-                                                     uint8_t* __restrict__ spp_out,
-                                                     float2* __restrict__ prev_pixel_out,
-                                                     float* __restrict__ acc_out,
-                                                     float* __restrict__ tone_out) {
-    constexpr int B = NS + FS + 3;
-    __shared__ FitLds<B> L;
-    const int t = threadIdx.x, g = blockIdx.x;
-    const int bx = g % P.blocks_x, by = g / P.blocks_x;
-
-    float a[B][kSubs];
-    f3 n_keep[kSubs], p_keep[kSubs];
-    float pfx[kSubs], pfy[kSubs];
-    long lin[kSubs];
-    uint32_t flags = 0;  // per s: bit 8s owner, bits 8s+1.. accept(4)
-    uint32_t spps = 0;
-#pragma unroll
-    for (int s = 0; s < kSubs; ++s) {
-        const int r = t + s * kLocal;
-        const int gx = bx * kEdge + (r & (kEdge - 1)), gy = by * kEdge + (r >> 5);
-        const NoisyItem it = noisy_item(P, in, cam, gx, gy, frame);
-#pragma unroll
-        for (int f = 0; f < B; ++f) {
-            const float v = design_value(P, f, it);
-            a[f][s] = HALF ? round_half(v) : v;
-        }
-        n_keep[s] = it.n;
-        p_keep[s] = it.p;
-        pfx[s] = it.pfx;
-        pfy[s] = it.pfy;
-        lin[s] = it.lin;
-        flags |= ((uint32_t)it.owner | ((uint32_t)it.accept << 1)) << (8 * s);
-        spps |= (uint32_t)it.spp << (8 * s);
-        if (it.owner) {
-            st3(noisy_out, it.lin, it.color);
-            spp_out[it.lin] = it.spp;
-            prev_pixel_out[it.lin] = make_float2(it.pfx, it.pfy);
-        }
-    }
-
-    fit_block<NS, FS, HALF, false, true>(a, L, t, frame, P.noise2);
-
-#pragma unroll
-    for (int s = 0; s < kSubs; ++s) {
-        const uint32_t fl = flags >> (8 * s);
-        if (fl & 1u) {
-            const f3 filtered = weighted_color(P, L.weights, L.minmax, n_keep[s], p_keep[s]);
-            const f3 acc = blend_filtered(P, filtered, pfx[s], pfy[s], (uint8_t)((fl >> 1) & 15u),
-                                          (uint8_t)(spps >> (8 * s)), acc_prev, frame);
-            st3(acc_out, lin[s], acc);
-            st3(tone_out, lin[s], tone_map(ld3(albedo, lin[s]), acc));
-        }
-    }
-}
-
 // ------------------------------------------------------------ noise table --
 // add_random()'s noise term (bmfr.cl:173-182) depends only on the row, the
 // feature and the frame, never on the block; K1 reads it from this table
@@ -340,22 +232,31 @@ hipError_t launch_accumulate_noisy(const Params& P, hipStream_t st, float2* prev
     return hipGetLastError();
 }
 
-template <int NS, int FS>
-static hipError_t launch_fitter_t(const Params& P, hipStream_t st, float* w, float* mm, void* tmp,
-                                  int frame) {
-    const int G = P.blocks_x * P.blocks_y;
-    if (P.half_tmp) hipLaunchKernelGGL((k_fitter<NS, FS, true>), dim3(G), dim3(256), 0, st, P, w, mm, tmp, frame);
-    else hipLaunchKernelGGL((k_fitter<NS, FS, false>), dim3(G), dim3(256), 0, st, P, w, mm, tmp, frame);
-    return hipGetLastError();
-}
-
-bool fitter_supported(int ns, int fs) { return ns == 4 && (fs == 6 || fs == 9); }
+// Feature counts with compiled kernels (bmfr_generic.h): FEATURES_NOT_SCALED
+// 1..4 (1.f and / or the normal components) x FEATURES_SCALED 0..9
+// (position monomials), any feature codes (bmfr.cpp:65-77); one translation
+// unit per FEATURES_NOT_SCALED (bmfr_generic_ns*.hip).
+bool fitter_supported(int ns, int fs) { return ns >= 1 && ns <= 4 && fs >= 0 && fs <= 9; }
 
 hipError_t launch_fitter(const Params& P, hipStream_t st, float* weights, float* mins_maxs, void* tmp,
                          int frame) {
-    if (P.not_scaled == 4 && P.scaled == 6) return launch_fitter_t<4, 6>(P, st, weights, mins_maxs, tmp, frame);
-    if (P.not_scaled == 4 && P.scaled == 9) return launch_fitter_t<4, 9>(P, st, weights, mins_maxs, tmp, frame);
-    return hipErrorInvalidValue;
+    switch (P.not_scaled) {
+        case 1: return launch_fitter_ns<1>(P, st, weights, mins_maxs, tmp, frame);
+        case 2: return launch_fitter_ns<2>(P, st, weights, mins_maxs, tmp, frame);
+        case 3: return launch_fitter_ns<3>(P, st, weights, mins_maxs, tmp, frame);
+        case 4: return launch_fitter_ns<4>(P, st, weights, mins_maxs, tmp, frame);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+static hipError_t launch_fused_generic(const Params& P, hipStream_t st, const FusedArgs& A) {
+    switch (P.not_scaled) {
+        case 1: return launch_fused_block_ns<1>(P, st, A);
+        case 2: return launch_fused_block_ns<2>(P, st, A);
+        case 3: return launch_fused_block_ns<3>(P, st, A);
+        case 4: return launch_fused_block_ns<4>(P, st, A);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_weighted_sum(const Params& P, hipStream_t st, const float* weights,
@@ -382,20 +283,6 @@ hipError_t launch_taa(const Params& P, hipStream_t st, const float2* prev_pixel,
     const dim3 blk(64, 4);
     hipLaunchKernelGGL(k_taa, grid2d(P.width, P.height, blk), blk, 0, st, P, prev_pixel, new_frame,
                        result, prev_frame, frame);
-    return hipGetLastError();
-}
-
-template <int NS, int FS>
-static hipError_t launch_fused_t(const Params& P, hipStream_t st, const FusedArgs& A) {
-    const int G = P.blocks_x * P.blocks_y;
-    if (P.half_tmp)
-        hipLaunchKernelGGL((k_fused_block<NS, FS, true>), dim3(G), dim3(256), 0, st, P, A.in, A.cam,
-                           A.frame, A.albedo, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out,
-                           A.acc_out, A.tone_out);
-    else
-        hipLaunchKernelGGL((k_fused_block<NS, FS, false>), dim3(G), dim3(256), 0, st, P, A.in, A.cam,
-                           A.frame, A.albedo, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out,
-                           A.acc_out, A.tone_out);
     return hipGetLastError();
 }
 
@@ -433,9 +320,7 @@ hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& 
         if (mid) (void)hipEventRecord(mid, st);
         return launch_fused_k2(P, st, A);
     }
-    if (P.not_scaled == 4 && P.scaled == 6) e = launch_fused_t<4, 6>(P, st, A);
-    else if (P.not_scaled == 4 && P.scaled == 9) e = launch_fused_t<4, 9>(P, st, A);
-    else return hipErrorInvalidValue;
+    e = launch_fused_generic(P, st, A);
     if (e != hipSuccess) return e;
     if (mid) (void)hipEventRecord(mid, st);
     return launch_taa(P, st, A.prev_pixel_out, A.tone_out, A.result_out, A.result_prev, A.frame);

@@ -109,7 +109,8 @@ class RefConfig:
 # Golden-vector configurations: small enough for the
 # pure-CPU oracle to run in seconds, covering height padding (80 -> 96),
 # width padding (100 -> 128), all 16 block offsets over 16 frames, both tmp
-# precisions and the 3rd-order feature set (B = 16).
+# precisions, the 3rd-order feature set (B = 16) and non-default feature
+# lists (B = 7, 10, 12; no scaled features).
 REF_CONFIGS = {
     c.name: c
     for c in (
@@ -119,6 +120,11 @@ REF_CONFIGS = {
         RefConfig("s96x64_f16", 96, 64, scaled=SCALED_THIRD_ORDER, half_tmp=0, frames=4),
         RefConfig("s48x48_h13", 48, 48, frames=4),
         RefConfig("s1280x720_h13", 1280, 720, frames=2),
+        # other feature lists (bmfr.cpp:65-77): generic-count kernels
+        RefConfig("s96x64_h7", 96, 64, not_scaled=(0,), scaled=(4, 5, 6), frames=4),
+        RefConfig("s96x64_f10", 96, 64, scaled=(4, 5, 6), half_tmp=0, frames=4),
+        RefConfig("s80x64_h12", 80, 64, not_scaled=(0, 3), scaled=(10, 11, 12, 7, 8, 9, 4), frames=4),
+        RefConfig("s64x64_h7", 64, 64, scaled=(), frames=3),
     )
 }
 
