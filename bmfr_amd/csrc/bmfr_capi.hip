@@ -26,7 +26,7 @@ struct bmfr_ctx {
     uint8_t* spp[2] = {nullptr, nullptr};
     float* acc[2] = {nullptr, nullptr};
     float* result[2] = {nullptr, nullptr};
-    float* tone = nullptr;
+    float* tone[2] = {nullptr, nullptr};  // K1-tone-mapped variants only
     float2* prev_pixel[2] = {nullptr, nullptr};  // double-buffered: K2 of frame f reads it while K1 of f+1 writes
     // bmfr_process_sequence: side stream for K2 and a ring of ordering events
     hipStream_t side = nullptr;
@@ -131,6 +131,7 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
                       : std::strcmp(v, "block") == 0   ? 1
                       : std::strcmp(v, "k1tone") == 0  ? 2
                       : std::strcmp(v, "rows") == 0    ? 3
+                      : std::strcmp(v, "tonecols") == 0 ? 4
                                                        : 0;
     P.ox = s->region_x;
     P.oy = s->region_y;
@@ -285,7 +286,7 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
         if (e == hipSuccess) e = hipMalloc(&c->acc[i], px * 3 * sizeof(float));
         if (e == hipSuccess) e = hipMalloc(&c->result[i], px * 3 * sizeof(float));
     }
-    if (e == hipSuccess) e = hipMalloc(&c->tone, px * 3 * sizeof(float));
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipMalloc(&c->tone[i], px * 3 * sizeof(float));
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipMalloc(&c->prev_pixel[i], px * sizeof(float2));
     if (e == hipSuccess && std::getenv("BMFR_STAMPS"))
         e = hipMalloc(&c->stamps, (size_t)sz.blocks * 8 * sizeof(unsigned long long));
@@ -310,7 +311,7 @@ bmfr_status bmfr_destroy(bmfr_ctx* c) {
         for (int i = 0; i < 3 * c->prof_capacity; ++i) (void)hipEventDestroy(c->prof_events[i]);
     delete[] c->prof_events;
     delete[] c->prof_frames;
-    (void)hipFree(c->tone);
+    for (int i = 0; i < 2; ++i) (void)hipFree(c->tone[i]);
     for (int i = 0; i < 2; ++i) (void)hipFree(c->prev_pixel[i]);
     if (c->side) {
         (void)hipStreamDestroy(c->side);
@@ -438,7 +439,7 @@ bmfr::FusedArgs frame_args(const bmfr_ctx* c, const bmfr_frame_inputs* in, const
     A.spp_out = c->spp[cur];
     A.prev_pixel_out = c->prev_pixel[cur];
     A.acc_out = c->acc[cur];
-    A.tone_out = c->tone;
+    A.tone_out = c->tone[cur];
     A.result_out = c->result[cur];
     A.noise_table = c->noise_table;
     A.stamps = c->stamps;
@@ -560,7 +561,7 @@ bmfr_status bmfr_process_sequence(bmfr_ctx* c, void* stream, int count, const bm
     if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // tiles exchange a halo between frames
     const hipStream_t s = as_stream(stream);
     const size_t out_bytes = c->sizes.region_bytes;
-    const bool pipelined = bmfr::fused_supported(c->P) && !bmfr::k1_tone_maps(c->P);
+    const bool pipelined = bmfr::fused_supported(c->P);
     bmfr_status st;
     if (!pipelined) {  // frame after frame on `stream`
         for (int i = 0; i < count; ++i) {
@@ -706,7 +707,7 @@ bmfr_status bmfr_state(const bmfr_ctx* c, int previous, bmfr_state_view* out) {
     out->noisy_accumulated = c->noisy_acc[i];
     out->spp = c->spp[i];
     out->filtered_accumulated = c->acc[i];
-    out->tone_mapped = c->tone;
+    out->tone_mapped = c->tone[i];
     out->prev_frame_pixel = reinterpret_cast<float*>(c->prev_pixel[i]);
     out->accept = nullptr;  // the fused kernel keeps accept bits in registers
     out->result = c->result[i];

@@ -422,8 +422,10 @@ __device__ __forceinline__ void back_substitute(Lds<B>& L, int t) {
 #ifndef BMFR_COLS_WAVES
 #define BMFR_COLS_WAVES 1  // minimum waves per SIMD requested from the register allocator
 #endif
-template <int NS, int FS, class IN>
+template <int NS, int FS, class IN, bool TONE>
 __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params P, NoisyInputs in, Camera cam, int frame,
+                                                          const float* __restrict__ albedo,
+                                                          float* __restrict__ tone_out,
                                                           const float* __restrict__ acc_prev,
                                                           float* __restrict__ noisy_out,
                                                           uint8_t* __restrict__ spp_out,
@@ -605,6 +607,7 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 #endif
             const f3 acc{alpha * ci.x + beta * prev.x, alpha * ci.y + beta * prev.y, alpha * ci.z + beta * prev.z};
             st3(acc_out, lin[i], acc);
+            if constexpr (TONE) st3(tone_out, lin[i], tone_map(ld3in<IN>(albedo, lin[i]), acc));  // bmfr.cl:851-856
         }
     }
 #ifdef BMFR_STAMPS
@@ -617,14 +620,19 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 }  // namespace cols
 
 bool fused_cols_supported(const Params& P) {
-    return P.half_tmp && P.fused_variant == 0 && fused_supported(P);
+    return P.half_tmp && (P.fused_variant == 0 || P.fused_variant == 4) && fused_supported(P);
 }
 
 template <int FS, class IN>
 static void launch_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
-    hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN>), dim3(P.nbx * P.nby), dim3(cols::kThreads), 0, st, P, A.in,
-                       A.cam, A.frame, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out, A.acc_out,
-                       A.noise_table, A.stamps);
+    if (k1_tone_maps(P))
+        hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, true>), dim3(P.nbx * P.nby), dim3(cols::kThreads), 0, st, P,
+                           A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
+                           A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
+    else
+        hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, false>), dim3(P.nbx * P.nby), dim3(cols::kThreads), 0, st,
+                           P, A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
+                           A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
 }
 
 hipError_t launch_fused_k1_cols(const Params& P, hipStream_t st, const FusedArgs& A) {

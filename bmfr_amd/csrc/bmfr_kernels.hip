@@ -200,6 +200,34 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
     }
 }
 
+// ------------------------------------------------ stencil K2 (tonecols) --
+// TAA straight from K1's tone-mapped frame in global memory, one pixel per
+// thread over the output tile, no LDS: light enough (<= 64 VGPRs) to run
+// beside four resident K1 blocks per CU.  Border work-groups check every
+// neighbour (bmfr.cl:901); interior ones skip the tests.
+__global__ __launch_bounds__(256, 8) void k_taa_stencil(Params P, const float* __restrict__ tone,
+                                                     const float2* __restrict__ prev_pixel,
+                                                     float* __restrict__ result,
+                                                     const float* __restrict__ prev_frame, int frame) {
+    const int x0 = P.tx0 + blockIdx.x * blockDim.x, y0 = P.ty0 + blockIdx.y * blockDim.y;
+    const int x = x0 + threadIdx.x, y = y0 + threadIdx.y;
+    if (x >= P.tx1 || y >= P.ty1) return;
+    const long lin = pix(P, x, y);
+    const float2 pf = prev_pixel[lin];
+    f3 pc[4];
+    taa_load_taps(P, pf, prev_frame, pc);
+    const f3 me = ld3(tone, lin);
+    f3 nb[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k)  // out-of-image neighbours: a clamped in-image pixel, skipped by taa_resolve
+        nb[k] = k == 4 ? rgb_to_ycocg(me)
+                       : rgb_to_ycocg(ld3(tone, pix(P, min(max(x + k % 3 - 1, 0), P.width - 1),
+                                                    min(max(y + k / 3 - 1, 0), P.height - 1))));
+    const bool edge = x0 == 0 || y0 == 0 || x0 + (int)blockDim.x >= P.width || y0 + (int)blockDim.y >= P.height;
+    st3(result, lin, edge ? taa_resolve<true>(P, x, y, me, pf, nb, pc, frame)
+                          : taa_resolve<false>(P, x, y, me, pf, nb, pc, frame));
+}
+
 // ------------------------------------------------------------ noise table --
 // add_random()'s noise term (bmfr.cl:173-182) depends only on the row, the
 // feature and the frame, never on the block; K1 reads it from this table
@@ -300,7 +328,12 @@ hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedAr
 
 hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A) {
     const dim3 grd((P.tx1 - P.tx0 + kTaaW - 1) / kTaaW, (P.ty1 - P.ty0 + kTaaH - 1) / kTaaH);
-    if (k1_tone_maps(P))
+    if (k2_stencil(P)) {
+        const dim3 blk(64, 4);
+        const dim3 g((P.tx1 - P.tx0 + 63) / 64, (P.ty1 - P.ty0 + 3) / 4);
+        hipLaunchKernelGGL(k_taa_stencil, g, blk, 0, st, P, A.tone_out, A.prev_pixel_out, A.result_out,
+                           A.result_prev, A.frame);
+    } else if (k1_tone_maps(P))
         hipLaunchKernelGGL((k_fused_taa<false, float>), grd, dim3(256), 0, st, P, A.tone_out, A.albedo,
                            A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
     else if (P.input_half)

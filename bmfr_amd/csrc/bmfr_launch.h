@@ -31,7 +31,11 @@ bool fused_supported(const Params& P);
 // pixel + halo (default: K1 is latency-bound and its VALU is the critical
 // resource; measured 0.68 vs 0.74 ms/frame at 4K), or in K1 for each owned
 // pixel, writing a tone-mapped frame (BMFR_FUSED_KERNEL=k1tone).
-inline bool k1_tone_maps(const Params& P) { return P.fused_variant == 2; }
+// BMFR_FUSED_KERNEL=tonecols: column-split K1 tone-maps its owned pixels
+// and K2 is a register-only stencil (k_taa_stencil: no LDS, <= 64 VGPRs) that
+// fits beside four resident K1 blocks on a CU (bmfr_process_sequence).
+inline bool k1_tone_maps(const Params& P) { return P.fused_variant == 2 || P.fused_variant == 4; }
+inline bool k2_stencil(const Params& P) { return P.fused_variant == 4; }
 hipError_t launch_fused_k1(const Params& P, hipStream_t st, const FusedArgs& A);
 // Column-split K1 (bmfr_fused_cols.hip): default for half tmp_data.
 bool fused_cols_supported(const Params& P);
