@@ -236,6 +236,26 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     }
 
 
+def valu_issue():
+    """VALU view of both kernels from the committed rocprofv3 SQ pass
+    (profiles/r01_sq_counters.json): instructions per SIMD x the achievable
+    issue cost of a wave64 f32 instruction (3.24 cycles, profiles/r01_valu_rate.txt)
+    / the kernel's cycles -- the fraction of the VALU roof each kernel uses."""
+    p = os.path.join(ROOT, "profiles", "r01_sq_counters.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    out = {}
+    for name, k in (("fused_block_k1", "K1 k_fused_cols"), ("taa_k2", "K2 k_fused_taa")):
+        if k in d:
+            c = d[k]
+            out[name] = round(c["valu_instr_per_simd"] * 3.24 / c["kernel_cycles_per_xcd"], 3)
+    out["source"] = "rocprofv3 SQ_INSTS_VALU / GRBM_GUI_ACTIVE (profiles/r01_sq_counters.json), " \
+                    "3.24 cycles per wave64 VALU instruction (tools/valu_rate.hip)"
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -310,6 +330,8 @@ def main():
                 "value": round(r1080["ms_per_frame"], 4), "device_ms_per_frame": round(r1080["dev_ms"], 4),
                 "kernel_ms": {"fused_block_k1": round(r1080["k1_ms"], 4), "taa_k2": round(r1080["k2_ms"], 4)},
                 "psnr_db": round(r1080["psnr"], 2)}
+        if world == 1:
+            line["valu_issue_frac"] = valu_issue()
         if world == 1 and a.cpu_frames > 0:
             line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_frames, a.seed)
         print(json.dumps(line), flush=True)

@@ -67,9 +67,12 @@ def main():
             print(f"{k:40s} {sys.argv[3]} {v:12.0f} KB  counted/true {v / true_kb:.3f}")
     elif cmd == "traffic":
         fetch_dir, write_dir, workload, px, alg = sys.argv[2:7]
-        k1 = os.environ.get("K1_NAME", "k_fused_cols<4, 6>")
-        f = pmc(fetch_dir, "FETCH_SIZE")[k1]
-        w = pmc(write_dir, "WRITE_SIZE")[k1]
+        k1 = os.environ.get("K1_NAME", "k_fused_cols<4, 6")
+
+        def pick(d):
+            return next(v for k, v in d.items() if k.startswith(k1))
+        f = pick(pmc(fetch_dir, "FETCH_SIZE"))
+        w = pick(pmc(write_dir, "WRITE_SIZE"))
         entry = {"fetch_kb_raw": f, "write_kb": w,
                  "hbm_bytes_per_launch": (2 * f + w) * 1024,
                  "hbm_bytes_per_launch_raw": (f + w) * 1024,
