@@ -135,6 +135,30 @@ __device__ __forceinline__ float vmax(float a, float b) {
     asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+// min(min(a, b), c) / max(max(a, b), c) in one instruction: bit for bit the
+// nested two-operand forms on gfx950 for every input incl. signed zeros,
+// infinities, quiet NaNs and denormals (tools/minmax3_check.hip, 64M triples).
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// The same with a wave-uniform first operand (a constant kept in an SGPR).
+__device__ __forceinline__ float vmin3s(float s, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "s"(s), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float vmax3s(float s, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "s"(s), "v"(b), "v"(c));
+    return r;
+}
 
 extern "C" __device__ float __ocml_powr_f32(float, float);
 

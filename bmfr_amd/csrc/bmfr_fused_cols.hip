@@ -46,6 +46,12 @@ constexpr int kUStride = 20;  // floats per lane in a u buffer: 16 + 4 (conflict
 // 96 VGPRs cost).
 #define BMFR_PARK_GLOBAL 0
 #endif
+#ifndef BMFR_P3_TAPS
+// 1: the filtered colour's taps are read in phase 3 instead (blend_filtered,
+// from the prev-frame pixel this thread stored in phase 1): no hand-over at
+// all, fewer phase-1 registers, one more dependent round trip in phase 3.
+#define BMFR_P3_TAPS 0
+#endif
 
 template <int B>
 struct Lds {
@@ -53,7 +59,7 @@ struct Lds {
         _Float16 M[B - 1][64 * kSlots];  // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
         float u[2][64 * kUStride];       // Householder vectors, double-buffered by column parity
     };
-#if !BMFR_PARK_GLOBAL
+#if !BMFR_PARK_GLOBAL && !BMFR_P3_TAPS
     float keep[4][3][kThreads];  // phase 1 -> 3: previous accumulated filtered colour per item
 #endif
     float piv[2][2];                    // |u|^2 and RN(1/|u|^2) of the published vector
@@ -472,7 +478,7 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 #pragma unroll
         for (int k = 0; k < PB; ++k) {
             const int i = i0 + k;
-            const NoisyItem it = noisy_item_spec<true, IN>(P, in, cam, cur[k], frame, acc_prev);
+            const NoisyItem it = noisy_item_spec<!BMFR_P3_TAPS, IN>(P, in, cam, cur[k], frame, acc_prev);
 #pragma unroll
             for (int f = 1; f < B; ++f) {
                 float v;
@@ -488,7 +494,9 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
             }
             spps |= (uint32_t)it.spp << (8 * i);
             ibits |= ((uint32_t)it.owner << i) | ((uint32_t)it.prev_f_divided << (4 + i));
-#if BMFR_PARK_GLOBAL
+#if BMFR_P3_TAPS
+            ibits |= (uint32_t)it.accept << (8 + 4 * i);  // accepted taps (bmfr.cl:380-404)
+#elif BMFR_PARK_GLOBAL
             if (it.owner) st3(acc_out, it.lin, it.prev_f);
 #else
             L.keep[i][0][t] = it.prev_f.x;
@@ -594,6 +602,11 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
             ci.x = ci.x < 0.f ? 0.f : ci.x;
             ci.y = ci.y < 0.f ? 0.f : ci.y;
             ci.z = ci.z < 0.f ? 0.f : ci.z;
+#if BMFR_P3_TAPS
+            const float2 pf = prev_pixel_out[lin[i]];  // this thread's phase-1 store
+            const f3 acc = blend_filtered(P, ci, pf.x, pf.y, (uint8_t)((ibits >> (8 + 4 * i)) & 15u),
+                                          (uint8_t)((spps >> (8 * i)) & 255u), acc_prev, frame);
+#else
             // bmfr.cl:834-849: alpha from the current spp when the taps carried weight
             const float alpha = (ibits & (1u << (4 + i)))
                                     ? fmaxf(1.f / (float)((spps >> (8 * i)) & 255u), P.second_blend_alpha)
@@ -606,6 +619,7 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
             const f3 prev{L.keep[i][0][t3], L.keep[i][1][t3], L.keep[i][2][t3]};
 #endif
             const f3 acc{alpha * ci.x + beta * prev.x, alpha * ci.y + beta * prev.y, alpha * ci.z + beta * prev.z};
+#endif
             st3(acc_out, lin[i], acc);
             if constexpr (TONE) st3(tone_out, lin[i], tone_map(ld3in<IN>(albedo, lin[i]), acc));  // bmfr.cl:851-856
         }

@@ -621,25 +621,40 @@ __device__ __forceinline__ f3 taa_resolve(const Params& P, int x, int y, f3 me, 
     if (frame == 0 || flx < -1.f || fly < -1.f || flx >= (float)W || fly >= (float)H)
         return me;  // bmfr.cl:884-890 (compared as floats: no int overflow)
     const int ix = (int)flx, iy = (int)fly;
-    f3 mnb{INFINITY, INFINITY, INFINITY}, mnc = mnb;
-    f3 mxb{-INFINITY, -INFINITY, -INFINITY}, mxc = mxb;
+    // bmfr.cl:897-920: min / max over the 3x3 box and the cross, visited dy
+    // outer, dx inner.  A skipped neighbour enters as +inf / -inf; the
+    // three-operand min / max keep upstream's left-to-right order exactly.
+    f3 nlo[9], nhi[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {  // bmfr.cl:897-920, dy outer, dx inner
-        const int dx = k % 3 - 1, dy = k / 3 - 1;
-        f3 lo = nb[k], hi = nb[k];
+    for (int k = 0; k < 9; ++k) {
+        nlo[k] = nb[k];
+        nhi[k] = nb[k];
         if (CHECK) {
-            const int sx = x + dx, sy = y + dy;
+            const int sx = x + k % 3 - 1, sy = y + k / 3 - 1;
             const bool in = sx >= 0 && sy >= 0 && sx < W && sy < H;
-            lo = in ? lo : f3{INFINITY, INFINITY, INFINITY};
-            hi = in ? hi : f3{-INFINITY, -INFINITY, -INFINITY};
+            nlo[k] = in ? nlo[k] : f3{INFINITY, INFINITY, INFINITY};
+            nhi[k] = in ? nhi[k] : f3{-INFINITY, -INFINITY, -INFINITY};
         }
-        if (dx == 0 || dy == 0) {
-            mnc = f3{vmin(mnc.x, lo.x), vmin(mnc.y, lo.y), vmin(mnc.z, lo.z)};
-            mxc = f3{vmax(mxc.x, hi.x), vmax(mxc.y, hi.y), vmax(mxc.z, hi.z)};
-        }
-        mnb = f3{vmin(mnb.x, lo.x), vmin(mnb.y, lo.y), vmin(mnb.z, lo.z)};
-        mxb = f3{vmax(mxb.x, hi.x), vmax(mxb.y, hi.y), vmax(mxb.z, hi.z)};
     }
+    auto box_cross = [&](auto get, float& mnb_, float& mxb_, float& mnc_, float& mxc_) {
+        const float inf = INFINITY;
+        float m = vmin3s(inf, get(nlo[0]), get(nlo[1]));
+        m = vmin3(m, get(nlo[2]), get(nlo[3]));
+        m = vmin3(m, get(nlo[4]), get(nlo[5]));
+        m = vmin3(m, get(nlo[6]), get(nlo[7]));
+        mnb_ = vmin(m, get(nlo[8]));
+        float M = vmax3s(-inf, get(nhi[0]), get(nhi[1]));
+        M = vmax3(M, get(nhi[2]), get(nhi[3]));
+        M = vmax3(M, get(nhi[4]), get(nhi[5]));
+        M = vmax3(M, get(nhi[6]), get(nhi[7]));
+        mxb_ = vmax(M, get(nhi[8]));
+        mnc_ = vmin(vmin3(vmin3s(inf, get(nlo[1]), get(nlo[3])), get(nlo[4]), get(nlo[5])), get(nlo[7]));
+        mxc_ = vmax(vmax3(vmax3s(-inf, get(nhi[1]), get(nhi[3])), get(nhi[4]), get(nhi[5])), get(nhi[7]));
+    };
+    f3 mnb, mxb, mnc, mxc;
+    box_cross([](const f3& v) { return v.x; }, mnb.x, mxb.x, mnc.x, mxc.x);
+    box_cross([](const f3& v) { return v.y; }, mnb.y, mxb.y, mnc.y, mxc.y);
+    box_cross([](const f3& v) { return v.z; }, mnb.z, mxb.z, mnc.z, mxc.z);
     f3 prev{0.f, 0.f, 0.f};
     float total = 0.f;
     const float fx = pf.x - flx, fy = pf.y - fly;
