@@ -132,6 +132,7 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
                       : std::strcmp(v, "k1tone") == 0  ? 2
                       : std::strcmp(v, "rows") == 0    ? 3
                       : std::strcmp(v, "tonecols") == 0 ? 4
+                      : std::strcmp(v, "colstone") == 0 ? 5
                                                        : 0;
     P.ox = s->region_x;
     P.oy = s->region_y;

@@ -634,7 +634,8 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 }  // namespace cols
 
 bool fused_cols_supported(const Params& P) {
-    return P.half_tmp && (P.fused_variant == 0 || P.fused_variant == 4) && fused_supported(P);
+    return P.half_tmp && (P.fused_variant == 0 || P.fused_variant == 4 || P.fused_variant == 5) &&
+           fused_supported(P);
 }
 
 template <int FS, class IN>

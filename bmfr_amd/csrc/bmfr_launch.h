@@ -34,7 +34,10 @@ bool fused_supported(const Params& P);
 // BMFR_FUSED_KERNEL=tonecols: column-split K1 tone-maps its owned pixels
 // and K2 is a register-only stencil (k_taa_stencil: no LDS, <= 64 VGPRs) that
 // fits beside four resident K1 blocks on a CU (bmfr_process_sequence).
-inline bool k1_tone_maps(const Params& P) { return P.fused_variant == 2 || P.fused_variant == 4; }
+// BMFR_FUSED_KERNEL=colstone: column-split K1 tone-maps, K2 = LDS TAA on its frame.
+inline bool k1_tone_maps(const Params& P) {
+    return P.fused_variant == 2 || P.fused_variant == 4 || P.fused_variant == 5;
+}
 inline bool k2_stencil(const Params& P) { return P.fused_variant == 4; }
 hipError_t launch_fused_k1(const Params& P, hipStream_t st, const FusedArgs& A);
 // Column-split K1 (bmfr_fused_cols.hip): default for half tmp_data.

@@ -37,7 +37,8 @@ struct Params {
     int half_tmp;                 // USE_HALF_PRECISION_IN_TMP_DATA
     int input_half;               // bmfr_config.input_half: frame input planes are half3
     int fused_variant;            // 0 = default, 1 = generic-feature K1, 2 = tone map in K1, 3 = row-split K1,
-                                  // 4 = tone map in K1 + stencil K2 (A/B diagnostics)
+                                  // 4 = tone map in K1 + stencil K2, 5 = tone map in column-split K1
+                                  // + LDS K2 (A/B diagnostics)
     // Buffer region (multi-GPU tiles): every plane of the fused path holds the
     // image pixels [ox, ox + stride) x [oy, oy + rows), row stride `stride`.
     // Untiled: 0, 0, width, height -- the reference's layout.

@@ -52,7 +52,8 @@ def _run(variant, sequence, half_tmp):
 
 @pytest.mark.parametrize("variant,sequence,half_tmp", [
     ("tonecols", False, 1), ("tonecols", True, 1), ("tonecols", False, 0),
-    ("k1tone", False, 1), ("k1tone", True, 1), ("rows", False, 1)])
+    ("k1tone", False, 1), ("k1tone", True, 1), ("rows", False, 1), ("colstone", False, 1),
+    ("colstone", True, 1)])
 def test_variant_matches_default(variant, sequence, half_tmp, gpu):
     want = _run(None, False, half_tmp)
     got = _run(variant, sequence, half_tmp)
