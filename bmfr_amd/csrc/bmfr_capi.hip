@@ -32,7 +32,8 @@ struct bmfr_ctx {
     hipStream_t side = nullptr;
     static constexpr int kSeqEvents = 4;
     hipEvent_t seq_k1[kSeqEvents] = {}, seq_k2[kSeqEvents] = {}, seq_start = nullptr;
-    double* noise_table = nullptr;
+    double* noise_table = nullptr;  // kNoiseFrames consecutive frames' tables from noise_first
+    int noise_first = -1;
     unsigned long long* stamps = nullptr;  // diagnostic: BMFR_STAMPS=1 with libbmfr_diag.so
     int cur = 0;
     bool has_frame = false;
@@ -291,7 +292,9 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipMalloc(&c->prev_pixel[i], px * sizeof(float2));
     if (e == hipSuccess && std::getenv("BMFR_STAMPS"))
         e = hipMalloc(&c->stamps, (size_t)sz.blocks * 8 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&c->noise_table, (size_t)bmfr::kMaxFeatures * bmfr::kBlockPixels * sizeof(double));
+    if (e == hipSuccess)
+        e = hipMalloc(&c->noise_table,
+                      (size_t)bmfr::kNoiseFrames * bmfr::kMaxFeatures * bmfr::kBlockPixels * sizeof(double));
     if (e != hipSuccess) {
         bmfr_destroy(c);
         return hip_status(e);
@@ -494,6 +497,21 @@ Params block_rect(Params P, int x0, int x1, int y0, int y1) {
     return P;
 }
 
+// Frame f's noise table (k_noise_table), made kNoiseFrames frames at a time on
+// stream s when f is outside the cached range.  Frames are ordered on their
+// streams by their state dependencies, so a batch is never rewritten under a
+// K1 that still reads it.
+hipError_t noise_for_frame(bmfr_ctx* c, const Params& P, hipStream_t s, int f, double** out) {
+    const size_t per = (size_t)(P.buffers - 4) * bmfr::kBlockPixels;
+    if (c->noise_first < 0 || f < c->noise_first || f >= c->noise_first + bmfr::kNoiseFrames) {
+        const hipError_t e = bmfr::launch_noise_tables(P, s, f, bmfr::kNoiseFrames, c->noise_table);
+        if (e != hipSuccess) return e;
+        c->noise_first = f;
+    }
+    *out = c->noise_table + (size_t)(f - c->noise_first) * per;
+    return hipSuccess;
+}
+
 // PART 0: noise table + interior blocks.  PART 1: border blocks + K2 (+ swap).
 // PART 2: everything (bmfr_process_frame).
 bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in, const float* m,
@@ -504,7 +522,7 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
     if (part != 1 && c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
     const hipStream_t s = as_stream(stream);
     const int cur = c->has_frame ? 1 - c->cur : 0;  // swap, bmfr.cpp:482-484
-    const bmfr::FusedArgs A = frame_args(c, in, m, off, frame_number, cur);
+    bmfr::FusedArgs A = frame_args(c, in, m, off, frame_number, cur);
     const Params P = frame_params(c, frame_number);
     if (part != 2 && !bmfr::fused_supported(P)) return BMFR_ERROR_UNSUPPORTED;
     hipEvent_t* ev = nullptr;
@@ -518,13 +536,16 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
         ++c->prof_count;
     }
     if (part == 2) {
+        if (bmfr::fused_supported(P) && (st = hip_status(noise_for_frame(c, P, s, frame_number, &A.noise_table))))
+            return st;
         st = hip_status(bmfr::launch_fused_frame(P, s, A, ev ? ev[1] : nullptr));
         if (st != BMFR_OK) return st;
     } else {
         int ix0, ix1, iy0, iy1;
         interior_blocks(c, P, frame_number, &ix0, &ix1, &iy0, &iy1);
+        // part 0 makes the table if needed, part 1 finds it in the cached range
+        if ((st = hip_status(noise_for_frame(c, P, s, frame_number, &A.noise_table))) != BMFR_OK) return st;
         if (part == 0) {
-            if ((st = hip_status(bmfr::launch_noise_table(P, s, A))) != BMFR_OK) return st;
             st = hip_status(bmfr::launch_fused_k1_blocks(block_rect(P, ix0, ix1, iy0, iy1), s, A));
             if (st != BMFR_OK) return st;
             c->pending_frame = frame_number;
@@ -601,8 +622,8 @@ bmfr_status bmfr_process_sequence(bmfr_ctx* c, void* stream, int count, const bm
     for (int i = 0; i < count; ++i) {
         const int f = first_frame + i;
         const int cur = c->has_frame ? 1 - c->cur : 0;
-        const bmfr::FusedArgs A = frame_args(c, &in[i], prev_frame_camera_matrices + 16 * i, pixel_offsets + 2 * i,
-                                             f, cur);
+        bmfr::FusedArgs A = frame_args(c, &in[i], prev_frame_camera_matrices + 16 * i, pixel_offsets + 2 * i,
+                                       f, cur);
         const Params P = frame_params(c, f);
         hipEvent_t* ev = nullptr;
         if (c->prof_capacity > 0) {
@@ -614,7 +635,7 @@ bmfr_status bmfr_process_sequence(bmfr_ctx* c, void* stream, int count, const bm
         const int k = i % bmfr_ctx::kSeqEvents;
         if (i >= 2) e = hipStreamWaitEvent(s, c->seq_k2[(i - 2) % bmfr_ctx::kSeqEvents], 0);
         if (ev && e == hipSuccess) e = hipEventRecord(ev[0], s);
-        if (e == hipSuccess) e = bmfr::launch_noise_table(P, s, A);
+        if (e == hipSuccess) e = noise_for_frame(c, P, s, f, &A.noise_table);
         if (e == hipSuccess) e = bmfr::launch_fused_k1_blocks(P, s, A);
         if (ev && e == hipSuccess) e = hipEventRecord(ev[1], s);
         if (e == hipSuccess) e = hipEventRecord(c->seq_k1[k], s);

@@ -233,11 +233,15 @@ __global__ __launch_bounds__(256, 8) void k_taa_stencil(Params P, const float* _
 // feature and the frame, never on the block; K1 reads it from this table
 // instead of re-hashing per element: table[(fb-1)*1024 + row] = random() - 0.5f
 // for fb = 1..B-4; the kernel forms NOISE_AMOUNT*2.f*that in double as upstream.
-__global__ __launch_bounds__(256) void k_noise_table(int frame, int buffers, double noise2,
+// Tables of `frames` consecutive frames from `first` are made in one launch
+// (one per kNoiseFrames frames), frame first + k at table + k * per_frame.
+__global__ __launch_bounds__(256) void k_noise_table(int first, int frames, int buffers, double noise2,
                                                      double* __restrict__ table) {
+    const int per_frame = (buffers - 4) * kBlockPixels;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (buffers - 4) * kBlockPixels) return;
-    const int fb = 1 + i / kBlockPixels, r = i % kBlockPixels;
+    if (i >= frames * per_frame) return;
+    const int frame = first + i / per_frame, j = i % per_frame;
+    const int fb = 1 + j / kBlockPixels, r = j % kBlockPixels;
     // add_random's addend (bmfr.cl:173-182) for row r of feature fb: the same
     // for every block, so computed once per frame.
     table[i] = noise2 * (double)(hash_random((uint32_t)(r + fb * kBlockPixels + frame * buffers * kBlockPixels)) - 0.5f);
@@ -314,11 +318,15 @@ hipError_t launch_taa(const Params& P, hipStream_t st, const float2* prev_pixel,
     return hipGetLastError();
 }
 
-hipError_t launch_noise_table(const Params& P, hipStream_t st, const FusedArgs& A) {
-    const int n = (P.buffers - 4) * kBlockPixels;
-    hipLaunchKernelGGL(k_noise_table, dim3((n + 255) / 256), dim3(256), 0, st, A.frame, P.buffers, P.noise2,
-                       A.noise_table);
+hipError_t launch_noise_tables(const Params& P, hipStream_t st, int first, int frames, double* table) {
+    const int n = frames * (P.buffers - 4) * kBlockPixels;
+    hipLaunchKernelGGL(k_noise_table, dim3((n + 255) / 256), dim3(256), 0, st, first, frames, P.buffers, P.noise2,
+                       table);
     return hipGetLastError();
+}
+
+hipError_t launch_noise_table(const Params& P, hipStream_t st, const FusedArgs& A) {
+    return launch_noise_tables(P, st, A.frame, 1, A.noise_table);
 }
 
 hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedArgs& A) {
@@ -348,7 +356,6 @@ hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A) 
 hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& A, hipEvent_t mid) {
     hipError_t e;
     if (fused_supported(P)) {
-        if ((e = launch_noise_table(P, st, A)) != hipSuccess) return e;
         if ((e = launch_fused_k1_blocks(P, st, A)) != hipSuccess) return e;
         if (mid) (void)hipEventRecord(mid, st);
         return launch_fused_k2(P, st, A);

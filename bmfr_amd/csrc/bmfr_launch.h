@@ -61,6 +61,9 @@ hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& 
 // noise table, K1 over the block rectangle of P (bx0, by0, nbx, nby; empty:
 // nothing), K2 over P's output tile.
 hipError_t launch_noise_table(const Params& P, hipStream_t st, const FusedArgs& A);
+// Noise tables of frames first .. first+frames-1, back to back from `table`.
+constexpr int kNoiseFrames = 64;
+hipError_t launch_noise_tables(const Params& P, hipStream_t st, int first, int frames, double* table);
 hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedArgs& A);
 hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A);
 hipError_t launch_taa(const Params& P, hipStream_t st, const float2* prev_pixel, const float* new_frame,
