@@ -551,11 +551,14 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
             c->pending_frame = frame_number;
             return BMFR_OK;
         }
-        const int x0 = P.bx0, x1 = P.bx0 + P.nbx, y0 = P.by0, y1 = P.by0 + P.nby;
-        const Params strips[4] = {block_rect(P, x0, x1, y0, iy0), block_rect(P, x0, x1, iy1, y1),
-                                  block_rect(P, x0, ix0, iy0, iy1), block_rect(P, ix1, x1, iy0, iy1)};
-        for (const Params& S : strips)  // an empty interior leaves the whole launch in strips[0]
-            if ((st = hip_status(bmfr::launch_fused_k1_blocks(S, s, A))) != BMFR_OK) return st;
+        // The border ring in one launch (an empty interior leaves the whole rectangle).
+        Params R = P;
+        if (ix1 > ix0 && iy1 > iy0) {
+            R.ring = P.nbx * P.nby - (ix1 - ix0) * (iy1 - iy0);
+            if (R.ring == 0) R.ring = -1;  // nothing outside the interior
+            R.rx0 = ix0, R.rx1 = ix1, R.ry0 = iy0, R.ry1 = iy1;
+        }
+        if ((st = hip_status(bmfr::launch_fused_k1_blocks(R, s, A))) != BMFR_OK) return st;
         if (ev) (void)hipEventRecord(ev[1], s);
         if ((st = hip_status(bmfr::launch_fused_k2(P, s, A))) != BMFR_OK) return st;
         c->pending_frame = -1;

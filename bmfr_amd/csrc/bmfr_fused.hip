@@ -326,7 +326,8 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
 #define BMFR_STAMP(k) (void)stamps
 #endif
     BMFR_STAMP(0);
-    const int bx = P.bx0 + g % P.nbx, by = P.by0 + g / P.nbx;
+    int bx, by;
+    k1_block(P, g, bx, by);
 
     // ---- accumulate_noisy_data (bmfr.cl:310-484) for rows t + 256s ----
     Rows<B, HALF> A;
@@ -476,11 +477,11 @@ bool fused_supported(const Params& P) {
 template <int NS, int FS, bool HALF, class IN>
 static void launch_k1(const Params& P, hipStream_t st, const FusedArgs& A) {
     if (k1_tone_maps(P))
-        hipLaunchKernelGGL((k_fused<NS, FS, HALF, true, IN>), dim3(P.nbx * P.nby), dim3(kThreads), 0, st, P,
+        hipLaunchKernelGGL((k_fused<NS, FS, HALF, true, IN>), dim3(k1_blocks(P)), dim3(kThreads), 0, st, P,
                            A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
                            A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
     else
-        hipLaunchKernelGGL((k_fused<NS, FS, HALF, false, IN>), dim3(P.nbx * P.nby), dim3(kThreads), 0, st, P,
+        hipLaunchKernelGGL((k_fused<NS, FS, HALF, false, IN>), dim3(k1_blocks(P)), dim3(kThreads), 0, st, P,
                            A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
                            A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
 }

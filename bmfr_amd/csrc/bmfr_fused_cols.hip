@@ -456,7 +456,8 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 #define BMFR_STAMP(k) (void)stamps
 #endif
     BMFR_STAMP(0);
-    const int bx = P.bx0 + g % P.nbx, by = P.by0 + g / P.nbx;
+    int bx, by;
+    k1_block(P, g, bx, by);
     const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
 
     // ---- accumulate_noisy_data (bmfr.cl:310-484), rows l + 64 (4w + i) ----
@@ -641,11 +642,11 @@ bool fused_cols_supported(const Params& P) {
 template <int FS, class IN>
 static void launch_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
     if (k1_tone_maps(P))
-        hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, true>), dim3(P.nbx * P.nby), dim3(cols::kThreads), 0, st, P,
+        hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, true>), dim3(k1_blocks(P)), dim3(cols::kThreads), 0, st, P,
                            A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
                            A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
     else
-        hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, false>), dim3(P.nbx * P.nby), dim3(cols::kThreads), 0, st,
+        hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, false>), dim3(k1_blocks(P)), dim3(cols::kThreads), 0, st,
                            P, A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
                            A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
 }

@@ -119,6 +119,35 @@ __device__ __forceinline__ int xcd_swizzle(int g, int G) {
     return xcd < rem ? xcd * (per + 1) + k : rem * (per + 1) + (xcd - rem) * per + k;
 }
 
+// Block (bx, by) of K1 work-group g: row-major over the launch rectangle, or
+// (ring launches) over its part outside the inner rectangle -- full rows
+// above it, the left and right pieces of the rows beside it, full rows below.
+__device__ __forceinline__ void k1_block(const Params& P, int g, int& bx, int& by) {
+    if (P.ring == 0) {
+        bx = P.bx0 + g % P.nbx;
+        by = P.by0 + g / P.nbx;
+        return;
+    }
+    const int W = P.nbx;
+    const int top = (P.ry0 - P.by0) * W;
+    if (g < top) {
+        bx = P.bx0 + g % W;
+        by = P.by0 + g / W;
+        return;
+    }
+    g -= top;
+    const int lw = P.rx0 - P.bx0, rw = P.bx0 + W - P.rx1, per_row = lw + rw, mid = (P.ry1 - P.ry0) * per_row;
+    if (g < mid) {
+        const int k = g % per_row;
+        by = P.ry0 + g / per_row;
+        bx = k < lw ? P.bx0 + k : P.rx1 + (k - lw);
+        return;
+    }
+    g -= mid;
+    bx = P.bx0 + g % W;
+    by = P.ry1 + g / W;
+}
+
 // Linear index of image pixel (x, y) in a plane of the buffer region, and
 // clamps into the region (= the image when untiled).
 __device__ __forceinline__ long pix(const Params& P, int x, int y) {

@@ -330,7 +330,7 @@ hipError_t launch_noise_table(const Params& P, hipStream_t st, const FusedArgs& 
 }
 
 hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedArgs& A) {
-    if (P.nbx <= 0 || P.nby <= 0) return hipSuccess;
+    if (P.nbx <= 0 || P.nby <= 0 || P.ring < 0) return hipSuccess;
     return fused_cols_supported(P) ? launch_fused_k1_cols(P, st, A) : launch_fused_k1(P, st, A);
 }
 

@@ -26,6 +26,8 @@ struct FusedArgs {
 };
 
 bool fitter_supported(int not_scaled, int scaled);
+// Work-groups of a K1 launch (the rectangle, or its ring).
+inline int k1_blocks(const Params& P) { return P.ring > 0 ? P.ring : P.nbx * P.nby; }
 bool fused_supported(const Params& P);
 // Where the canonical path tone-maps (bmfr.cl:851-856): in K2 for each tile
 // pixel + halo (default: K1 is latency-bound and its VALU is the critical

@@ -46,6 +46,10 @@ struct Params {
     // Per launch: the blocks of the shifted grid K1 covers (bx0 + g % nbx,
     // by0 + g / nbx) and the output tile [tx0, tx1) x [ty0, ty1) of K2.
     int bx0, by0, nbx, nby;
+    // ring > 0: the launch covers only the blocks of that rectangle outside
+    // the inner rectangle [rx0, rx1) x [ry0, ry1) (a tile's border ring,
+    // bmfr_process_frame_border), ring = their count.
+    int ring, rx0, ry0, rx1, ry1;
     int tx0, ty0, tx1, ty1;
 };
 
