@@ -178,14 +178,20 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         if transport is None or f == 0:
             den.process_frame(*args, **kw)
         elif not a.overlap:
-            transport.exchange(tiling.state_planes(den), copier)
+            if backend == "nccl":
+                transport.exchange_ctx(den)
+            else:
+                transport.exchange(tiling.state_planes(den), copier)
             den.process_frame(*args, **kw)
         else:
             planes = tiling.state_planes(den)  # the previous frame's state until _border
             comm.wait_event(frame_done)
             den.process_frame_interior(*args, **kw)
             with torch.cuda.stream(comm):
-                transport.exchange(planes, copier)
+                if backend == "nccl":  # one pack and one unpack kernel around the RCCL batch
+                    transport.exchange_ctx(den)
+                else:
+                    transport.exchange(planes, copier)
             compute.wait_stream(comm)
             den.process_frame_border(*args, **kw)
         if frame_done is not None:

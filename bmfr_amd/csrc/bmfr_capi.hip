@@ -667,6 +667,40 @@ bmfr_status bmfr_process_frame_border(bmfr_ctx* c, void* stream, const bmfr_fram
     return process_part(c, stream, in, prev_frame_camera_matrix, pixel_offset, frame_number, 1);
 }
 
+bmfr_status bmfr_halo_copy(bmfr_ctx* c, void* stream, const int* rects, int n, void* buffer, int unpack,
+                           size_t* bytes) {
+    if (!c || n < 0 || (n > 0 && !rects) || n * 4 > bmfr::kMaxHaloSegs) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (!is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
+    const int i = c->cur;  // bmfr_state(previous = 0): the last frame's state
+    struct {
+        uint8_t* base;
+        int bpp;
+    } planes[4] = {{reinterpret_cast<uint8_t*>(c->noisy_acc[i]), 12}, {c->spp[i], 1},
+                   {reinterpret_cast<uint8_t*>(c->acc[i]), 12}, {reinterpret_cast<uint8_t*>(c->result[i]), 12}};
+    const bmfr_sizes& s = c->sizes;
+    bmfr::HaloArgs a{};
+    long long off = 0;
+    for (int r = 0; r < n; ++r) {
+        const int x = rects[4 * r], y = rects[4 * r + 1], w = rects[4 * r + 2], h = rects[4 * r + 3];
+        if (w <= 0 || h <= 0 || x < s.region_x || y < s.region_y || x + w > s.region_x + s.region_width ||
+            y + h > s.region_y + s.region_height)
+            return BMFR_ERROR_INVALID_ARGUMENT;
+        for (const auto& p : planes) {
+            bmfr::HaloSeg& g = a.seg[a.nseg++];
+            const size_t first = ((size_t)(y - s.region_y) * s.region_width + (x - s.region_x)) * p.bpp;
+            g.plane = reinterpret_cast<unsigned long long>(p.base + first);
+            g.buf_off = off;
+            g.row_bytes = w * p.bpp;
+            g.rows = h;
+            g.pitch = s.region_width * p.bpp;
+            off += ((long long)g.row_bytes * h + 15) & ~15LL;
+        }
+    }
+    if (bytes) *bytes = (size_t)off;
+    if (!buffer) return BMFR_OK;
+    return hip_status(bmfr::launch_halo_copy(a, as_stream(stream), buffer, unpack));
+}
+
 bmfr_status bmfr_set_profiling(bmfr_ctx* c, int enable, int capacity) {
     if (!c || (enable && capacity <= 0)) return BMFR_ERROR_INVALID_ARGUMENT;
     if (c->prof_events) {

@@ -228,6 +228,42 @@ __global__ __launch_bounds__(256, 8) void k_taa_stencil(Params P, const float* _
                           : taa_resolve<false>(P, x, y, me, pf, nb, pc, frame));
 }
 
+// ------------------------------------------------------------ halo copy --
+// Rectangles of state planes <-> one packed buffer (multi-GPU halo exchange),
+// all segments in one launch: blockIdx.y = segment.  Segments whose rows are
+// 4-byte multiples copy by dword, the rest (spp rows) by byte.
+__global__ __launch_bounds__(256) void k_halo_copy(HaloArgs a, uint8_t* __restrict__ buf, int unpack) {
+    const HaloSeg& s = a.seg[blockIdx.y];
+    uint8_t* plane = reinterpret_cast<uint8_t*>(s.plane);
+    uint8_t* packed = buf + s.buf_off;
+    const long total = (long)s.row_bytes * s.rows;
+    const bool words = (s.row_bytes & 3) == 0 && (s.pitch & 3) == 0 && (s.plane & 3) == 0;
+    const long stride = (long)gridDim.x * blockDim.x;
+    if (words) {
+        const int rw = s.row_bytes >> 2;
+        for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total / 4; i += stride) {
+            const long row = i / rw, col = i % rw;
+            uint32_t* p = reinterpret_cast<uint32_t*>(plane + row * s.pitch) + col;
+            uint32_t* q = reinterpret_cast<uint32_t*>(packed) + i;
+            if (unpack) *p = *q;
+            else *q = *p;
+        }
+    } else {
+        for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += stride) {
+            const long row = i / s.row_bytes, col = i % s.row_bytes;
+            uint8_t* p = plane + row * s.pitch + col;
+            if (unpack) *p = packed[i];
+            else packed[i] = *p;
+        }
+    }
+}
+
+hipError_t launch_halo_copy(const HaloArgs& a, hipStream_t st, void* buf, int unpack) {
+    if (a.nseg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_halo_copy, dim3(64, a.nseg), dim3(256), 0, st, a, static_cast<uint8_t*>(buf), unpack);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------ noise table --
 // add_random()'s noise term (bmfr.cl:173-182) depends only on the row, the
 // feature and the frame, never on the block; K1 reads it from this table

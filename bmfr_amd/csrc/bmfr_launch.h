@@ -7,6 +7,20 @@
 
 namespace bmfr {
 
+// Halo exchange: rectangle segments of state planes and their place in a
+// packed buffer (bmfr_halo_copy).
+struct HaloSeg {
+    unsigned long long plane;  // device address of the rectangle's first byte in the plane
+    long long buf_off;         // byte offset of the segment in the packed buffer (16-byte aligned)
+    int row_bytes, rows, pitch;
+};
+constexpr int kMaxHaloSegs = 64;
+struct HaloArgs {
+    HaloSeg seg[kMaxHaloSegs];
+    int nseg;
+};
+hipError_t launch_halo_copy(const HaloArgs& a, hipStream_t st, void* buf, int unpack);
+
 // Arguments of one fused frame (K1 + K2).
 struct FusedArgs {
     NoisyInputs in;

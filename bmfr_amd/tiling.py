@@ -168,6 +168,36 @@ def rect_bytes(planes, r: Rect | None) -> int:
     return 0 if r is None else sum(r[2] * r[3] * p.bpp for p in planes)
 
 
+# ------------------------------------------------- libbmfr halo copies ----
+def _rect_array(rects):
+    return (C.c_int * max(4 * len(rects), 1))(*[v for r in rects for v in r])
+
+
+def halo_bytes(denoiser, rects) -> list:
+    """Packed size of each rectangle's four state-plane segments (bmfr_halo_copy layout)."""
+    from ._lib import check
+    out = []
+    for r in rects:
+        n = C.c_size_t()
+        check(denoiser.lib.bmfr_halo_copy(denoiser.handle, None, _rect_array([r]), 1, None, 0, C.byref(n)),
+              "bmfr_halo_copy")
+        out.append(n.value)
+    return out
+
+
+def halo_copy(denoiser, rects, buf_ptr: int, unpack: bool, stream=None) -> None:
+    """Pack (or unpack) the rectangles of the state planes into (from) a device
+    buffer in one kernel launch on `stream` (torch stream; default current)."""
+    import torch
+
+    from ._lib import check
+    if not rects:
+        return
+    s = (stream or torch.cuda.current_stream()).cuda_stream
+    check(denoiser.lib.bmfr_halo_copy(denoiser.handle, s, _rect_array(rects), len(rects), buf_ptr, int(unpack),
+                                      None), "bmfr_halo_copy")
+
+
 # ------------------------------------------------------------- transports ----
 class DistTransport:
     """torch.distributed point-to-point: one grouped batch of isend/irecv per frame."""
@@ -188,6 +218,35 @@ class DistTransport:
             b = self.torch.empty(max(nbytes, 1), dtype=self.torch.uint8, device=device or self.device)
             self._bufs[key] = b
         return b
+
+    def exchange_ctx(self, denoiser) -> None:
+        """The exchange on a tiled Denoiser with libbmfr's one-launch pack and
+        unpack (bmfr_halo_copy) on the current stream: two kernels per frame
+        around one grouped isend/irecv batch (RCCL orders it on that stream)."""
+        import torch.distributed as dist
+        if not hasattr(self, "_layout"):
+            plan = self.grid.plan(self.rank)
+            sends = [(p, s) for p, s, _ in plan if s]
+            recvs = [(p, r) for p, _, r in plan if r]
+            self._layout = (sends, halo_bytes(denoiser, [s for _, s in sends]),
+                            recvs, halo_bytes(denoiser, [r for _, r in recvs]))
+        sends, s_sizes, recvs, r_sizes = self._layout
+        if not sends and not recvs:
+            return
+        sbuf = self.buffer("S", sum(s_sizes))
+        rbuf = self.buffer("R", sum(r_sizes))
+        halo_copy(denoiser, [s for _, s in sends], sbuf.data_ptr(), unpack=False)
+        ops, off = [], 0
+        for (peer, _), n in zip(sends, s_sizes):
+            ops.append(dist.P2POp(dist.isend, sbuf[off:off + n], peer))
+            off += n
+        off = 0
+        for (peer, _), n in zip(recvs, r_sizes):
+            ops.append(dist.P2POp(dist.irecv, rbuf[off:off + n], peer))
+            off += n
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        halo_copy(denoiser, [r for _, r in recvs], rbuf.data_ptr(), unpack=True)
 
     def exchange(self, planes, copier) -> None:
         import torch.distributed as dist
@@ -227,6 +286,20 @@ class LoopbackTransport:
 
     def __init__(self, grid: TileGrid):
         self.grid = grid
+
+    def exchange_all_ctx(self, denoisers) -> None:
+        """The same through libbmfr's pack / unpack kernels (bmfr_halo_copy):
+        each message packed from the sender's context and unpacked into the
+        receiver's, as DistTransport.exchange_ctx moves them."""
+        import torch
+        for rank in range(self.grid.ranks):
+            for peer, s, _ in self.grid.plan(rank):
+                if not s:
+                    continue
+                n = halo_bytes(denoisers[rank], [s])[0]
+                buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+                halo_copy(denoisers[rank], [s], buf.data_ptr(), unpack=False)
+                halo_copy(denoisers[peer], [s], buf.data_ptr(), unpack=True)
 
     def exchange_all(self, planes_by_rank, copier) -> None:
         for rank in range(self.grid.ranks):

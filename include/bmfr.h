@@ -223,6 +223,17 @@ bmfr_status bmfr_process_sequence(bmfr_ctx *ctx, void *stream, int count, const 
     const float *prev_frame_camera_matrices, const float *pixel_offsets, int first_frame,
     float *const *outputs);
 
+/* Halo exchange support for tiled contexts: copy the rectangles rects[n][4]
+ * = {x, y, width, height} (image coordinates inside the context's region) of
+ * the four exchanged state planes of bmfr_state(previous = 0) --
+ * noisy_accumulated (12 B/px), spp (1), filtered_accumulated (12), result
+ * (12) -- into (unpack = 0) or out of (unpack = 1) `buffer` (device memory),
+ * rectangle after rectangle, plane after plane, rows packed, each segment
+ * padded to 16 bytes; one kernel launch on `stream`.  *bytes (nullable)
+ * receives the packed size; buffer = NULL only computes it.  n <= 16. */
+bmfr_status bmfr_halo_copy(bmfr_ctx *ctx, void *stream, const int *rects, int n, void *buffer, int unpack,
+    size_t *bytes);
+
 /* Device pointer to the last processed frame's output (TAA result, float3,
  * W*H, the buffer the reference reads back at bmfr.cpp:479-480).  Valid until
  * the next bmfr_process_frame. */

@@ -28,8 +28,9 @@ def _tile_of(a: np.ndarray, region, tile, ch):
 
 @pytest.mark.parametrize("shape", [(320, 256, 2, 2, 40), (352, 224, 2, 1, 48), (256, 320, 1, 2, 40),
                                    (480, 288, 4, 2, 38)])
-@pytest.mark.parametrize("half,split", [(1, False), (0, False), (1, True)])
-def test_tiled_matches_untiled_bitwise(shape, half, split, gpu):
+@pytest.mark.parametrize("half,split,kernel_copy", [(1, False, False), (0, False, False), (1, True, False),
+                                                    (1, True, True)])
+def test_tiled_matches_untiled_bitwise(shape, half, split, kernel_copy, gpu):
     """split: each frame as bmfr_process_frame_interior, halo exchange,
     bmfr_process_frame_border -- with the halo ring poisoned (all-ones bytes:
     NaN colours, spp 255) until the exchange, so an interior block that read
@@ -68,7 +69,10 @@ def test_tiled_matches_untiled_bitwise(shape, half, split, gpu):
             for r in range(grid.ranks):
                 call("process_frame_interior", r)
             if f > 0:
-                loop.exchange_all([state_planes(d) for d in tiles], copier)
+                if kernel_copy:  # libbmfr's one-launch pack / unpack (bmfr_halo_copy)
+                    loop.exchange_all_ctx(tiles)
+                else:
+                    loop.exchange_all([state_planes(d) for d in tiles], copier)
             for r in range(grid.ranks):
                 call("process_frame_border", r)
         else:
