@@ -166,7 +166,6 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     # (bmfr_process_frame_interior / _border, include/bmfr.h).
     compute = torch.cuda.current_stream(dev)
     comm = torch.cuda.Stream(dev) if grid else None
-    copier = tiling.HipCopier(stream=comm.cuda_stream if (grid and a.overlap) else None) if grid else None
     frame_done = torch.cuda.Event() if grid else None
     torch.cuda.synchronize()
 
@@ -178,20 +177,13 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         if transport is None or f == 0:
             den.process_frame(*args, **kw)
         elif not a.overlap:
-            if backend == "nccl":
-                transport.exchange_ctx(den)
-            else:
-                transport.exchange(tiling.state_planes(den), copier)
+            transport.exchange_ctx(den)
             den.process_frame(*args, **kw)
         else:
-            planes = tiling.state_planes(den)  # the previous frame's state until _border
-            comm.wait_event(frame_done)
+            comm.wait_event(frame_done)  # the previous frame's state is complete
             den.process_frame_interior(*args, **kw)
-            with torch.cuda.stream(comm):
-                if backend == "nccl":  # one pack and one unpack kernel around the RCCL batch
-                    transport.exchange_ctx(den)
-                else:
-                    transport.exchange(planes, copier)
+            with torch.cuda.stream(comm):  # one pack and one unpack kernel around the RCCL batch
+                transport.exchange_ctx(den)
             compute.wait_stream(comm)
             den.process_frame_border(*args, **kw)
         if frame_done is not None:

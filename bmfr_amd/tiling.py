@@ -233,19 +233,27 @@ class DistTransport:
         sends, s_sizes, recvs, r_sizes = self._layout
         if not sends and not recvs:
             return
-        sbuf = self.buffer("S", sum(s_sizes))
-        rbuf = self.buffer("R", sum(r_sizes))
+        ns, nr = sum(s_sizes), sum(r_sizes)
+        sbuf = self.buffer("S", ns)
+        rbuf = self.buffer("R", nr)
         halo_copy(denoiser, [s for _, s in sends], sbuf.data_ptr(), unpack=False)
+        s_msg, r_msg = sbuf, rbuf
+        if self.host_staging:  # gloo: the messages travel through host memory
+            cpu = self.torch.device("cpu")
+            s_msg, r_msg = self.buffer("SH", ns, cpu), self.buffer("RH", nr, cpu)
+            s_msg[:ns].copy_(sbuf[:ns])  # synchronous device-to-host copy on the current stream
         ops, off = [], 0
         for (peer, _), n in zip(sends, s_sizes):
-            ops.append(dist.P2POp(dist.isend, sbuf[off:off + n], peer))
+            ops.append(dist.P2POp(dist.isend, s_msg[off:off + n], peer))
             off += n
         off = 0
         for (peer, _), n in zip(recvs, r_sizes):
-            ops.append(dist.P2POp(dist.irecv, rbuf[off:off + n], peer))
+            ops.append(dist.P2POp(dist.irecv, r_msg[off:off + n], peer))
             off += n
         for w in dist.batch_isend_irecv(ops):
             w.wait()
+        if self.host_staging:
+            rbuf[:nr].copy_(r_msg[:nr])
         halo_copy(denoiser, [r for _, r in recvs], rbuf.data_ptr(), unpack=True)
 
     def exchange(self, planes, copier) -> None:
