@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--third-order", action="store_true", help="B = 16 feature set (BASELINE config 5)")
     ap.add_argument("--input-half", action="store_true",
                     help="half3 input planes (BASELINE config 5's fp16 feature buffers)")
+    ap.add_argument("--library-powr", action="store_true",
+                    help="tone map with the device library's powr (bit-identical to the reference kernel "
+                         "on gfx950) instead of the correctly rounded one")
     ap.add_argument("--no-1080p", action="store_true", help="skip the 1920x1080 line (N = 1 only)")
     ap.add_argument("--cpu-frames", type=int, default=2, help="timed CPU-oracle frames (0 = skip)")
     ap.add_argument("--seed", type=int, default=0x424D4652)
@@ -140,7 +143,7 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, scaled=scaled,
                               use_half_precision_in_tmp_data=a.half_tmp,
                               tile=tile if grid else None, tile_halo=a.halo if grid else 0,
-                              input_half=int(a.input_half))
+                              input_half=int(a.input_half), library_powr=int(a.library_powr))
     local = dev.index
     den = bmfr_amd.Denoiser(cfg, device=local)
     region = den.region
@@ -315,7 +318,8 @@ def main():
             "dtype": "f32" + ("+f16 tmp_data" if a.half_tmp else "") + ("+f16 input planes" if a.input_half else ""),
             "data": "synthetic (GPU-rendered 1-spp frames + features, resident in HBM)",
             "config": {"workload": workload, "image": f"{W}x{H}", "buffer_count": cfg.buffer_count,
-                       "half_tmp_data": a.half_tmp, "input_half": int(a.input_half), "frames_timed": a.steps,
+                       "half_tmp_data": a.half_tmp, "input_half": int(a.input_half),
+                       "powr": "device library" if a.library_powr else "correctly rounded", "frames_timed": a.steps,
                        "frames_pipelined": world == 1 and a.sequence,
                        "parallelism": (f"tiles {tx}x{ty}, halo {a.halo} px, "
                                        f"{'RCCL' if backend == 'nccl' else backend} halo exchange"

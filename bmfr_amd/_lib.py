@@ -49,6 +49,7 @@ class Config(C.Structure):
         ("tile_x", C.c_int), ("tile_y", C.c_int), ("tile_width", C.c_int), ("tile_height", C.c_int),
         ("tile_halo", C.c_int),
         ("input_half", C.c_int),
+        ("library_powr", C.c_int),
     ]
 
 

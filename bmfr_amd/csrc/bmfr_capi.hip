@@ -124,6 +124,7 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     P.normal_limit_sq = as_kernel_literal(c->normal_limit_squared);
     P.half_tmp = c->use_half_precision_in_tmp_data ? 1 : 0;
     P.input_half = c->input_half ? 1 : 0;
+    P.library_powr = c->library_powr ? 1 : 0;
     // Diagnostic A/B overrides of the fused path: BMFR_FUSED_KERNEL=block
     // (generic-feature K1), k1tone (row-split K1 with tone mapping in K1) or
     // rows (row-split K1, bmfr_fused.hip, instead of the column-split one).

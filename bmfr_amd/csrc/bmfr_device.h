@@ -160,7 +160,6 @@ __device__ __forceinline__ float vmax3s(float s, float b, float c) {
     return r;
 }
 
-extern "C" __device__ float __ocml_powr_f32(float, float);
 
 // Correctly rounded a / b given y = RN(1/b): one Markstein correction step
 // (r = a - q*b is exact under FMA; q + r*y rounds to RN(a/b) when a, b, 1/b

@@ -457,7 +457,7 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
             const f3 acc = blend_filtered(P, c, pp[s].x, pp[s].y, (uint8_t)((bits[s] >> 1) & 15u),
                                           (uint8_t)(bits[s] >> 8), acc_prev, frame);
             st3(acc_out, lin[s], acc);
-            if (TONE) st3(tone_out, lin[s], tone_map(alb[s], acc));  // bmfr.cl:851-856
+            if (TONE) st3(tone_out, lin[s], tone_map(P, alb[s], acc));  // bmfr.cl:851-856
         }
     }
 #ifdef BMFR_STAMPS

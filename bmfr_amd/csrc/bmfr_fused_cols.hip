@@ -622,7 +622,7 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
             const f3 acc{alpha * ci.x + beta * prev.x, alpha * ci.y + beta * prev.y, alpha * ci.z + beta * prev.z};
 #endif
             st3(acc_out, lin[i], acc);
-            if constexpr (TONE) st3(tone_out, lin[i], tone_map(ld3in<IN>(albedo, lin[i]), acc));  // bmfr.cl:851-856
+            if constexpr (TONE) st3(tone_out, lin[i], tone_map(P, ld3in<IN>(albedo, lin[i]), acc));  // bmfr.cl:851-856
         }
     }
 #ifdef BMFR_STAMPS

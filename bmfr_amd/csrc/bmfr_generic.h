@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void k_fused_block(Params P, NoisyInputs in, C
             const f3 acc = blend_filtered(P, filtered, pfx[s], pfy[s], (uint8_t)((fl >> 1) & 15u),
                                           (uint8_t)(spps >> (8 * s)), acc_prev, frame);
             st3(acc_out, lin[s], acc);
-            st3(tone_out, lin[s], tone_map(ld3(albedo, lin[s]), acc));
+            st3(tone_out, lin[s], tone_map(P, ld3(albedo, lin[s]), acc));
         }
     }
 }

@@ -11,6 +11,7 @@
 #pragma once
 
 #include "bmfr_device.h"
+#include "bmfr_powr.h"
 
 namespace bmfr {
 
@@ -612,13 +613,18 @@ __device__ __forceinline__ f3 blend_filtered(const Params& P, f3 filtered, float
               alpha * filtered.z + beta * prev.z};
 }
 
-// Albedo remodulation + 1/2.2 gamma + clamp (bmfr.cl:851-856), with the
-// device library's powr exactly as the reference kernel calls it.
-__device__ __forceinline__ f3 tone_map(f3 albedo, f3 a) {
-    const float g = 0.454545f;
-    return f3{fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.x * a.x), g), 0.f), 1.f),
-              fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.y * a.y), g), 0.f), 1.f),
-              fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, albedo.z * a.z), g), 0.f), 1.f)};
+// Albedo remodulation + 1/2.2 gamma + clamp (bmfr.cl:851-856), with powr
+// correctly rounded (bmfr_powr.h: equal to the oracle's for every input) or,
+// with library_powr, the device library's as the reference kernel calls it.
+__device__ __forceinline__ f3 tone_map(const Params& P, f3 albedo, f3 a) {
+    const f3 p{albedo.x * a.x, albedo.y * a.y, albedo.z * a.z};
+    if (P.library_powr) {
+        const float g = 0.454545f;
+        return f3{fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, p.x), g), 0.f), 1.f),
+                  fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, p.y), g), 0.f), 1.f),
+                  fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, p.z), g), 0.f), 1.f)};
+    }
+    return f3{gamma_clamped(p.x), gamma_clamped(p.y), gamma_clamped(p.z)};
 }
 
 // The four bilinear taps of the previous TAA output at reprojected position

@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void k_accumulate_filtered(
     const f3 a = blend_filtered(P, ld3(filtered, lin), pp.x, pp.y, frame > 0 ? accept[lin] : 0, spp[lin],
                                 acc_prev, frame);
     st3(acc, lin, a);
-    st3(tone_mapped, lin, tone_map(ld3(albedo, lin), a));
+    st3(tone_mapped, lin, tone_map(P, ld3(albedo, lin), a));
 }
 
 // ---------------------------------------------------------------- stage 5 --
@@ -107,21 +107,33 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
 
 // --------------------------------------------------------- fused K2: TAA --
 // One 64x16 tile per 256-thread work-group.  The tile's tone-mapped colours
-// and a 1-pixel halo go to LDS once, as RGB and as YCoCg, and the 3x3
-// neighbourhoods (bmfr.cl:897-920) are read from there.  TONE: the tile is
-// tone-mapped here from the accumulated colour and the albedo (K1 then
-// writes no tone-mapped frame); otherwise K1's tone-mapped frame is read.
-constexpr int kTaaW = 64, kTaaH = 16;
+// and a 1-pixel halo go to LDS once as YCoCg, and the 3x3 neighbourhoods
+// (bmfr.cl:897-920) are read from there; each thread keeps the RGB of its own
+// four output pixels in registers.  TONE: the tile is tone-mapped here from
+// the accumulated colour and the albedo (K1 then writes no tone-mapped
+// frame); otherwise K1's tone-mapped frame is read.  19 KB of LDS per
+// work-group, so up to eight fit a CU.
+#ifndef BMFR_K2_H  // tile height (multiple of 4)
+#define BMFR_K2_H 16
+#endif
+constexpr int kTaaW = 64, kTaaH = BMFR_K2_H;
+#ifndef BMFR_K2_WAVES  // minimum waves per SIMD the register allocation must allow
+#define BMFR_K2_WAVES 1
+#endif
+#ifndef BMFR_K2_EARLY_TAPS  // previous-frame taps loaded before the tone map
+#define BMFR_K2_EARLY_TAPS 0
+#endif
 template <bool TONE, class IN>
-__global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __restrict__ src,
-                                                   const float* __restrict__ albedo,
-                                                   const float2* __restrict__ prev_pixel,
-                                                   float* __restrict__ result,
-                                                   const float* __restrict__ prev_frame, int frame) {
+__global__ __launch_bounds__(256, BMFR_K2_WAVES) void k_fused_taa(Params P, const float* __restrict__ src,
+                                                                  const float* __restrict__ albedo,
+                                                                  const float2* __restrict__ prev_pixel,
+                                                                  float* __restrict__ result,
+                                                                  const float* __restrict__ prev_frame,
+                                                                  int frame) {
     constexpr int HW = kTaaW + 2, HH = kTaaH + 2, N = HW * HH;
-    constexpr int ITER = (N + 255) / 256;
-    __shared__ float T[3][N];   // RGB (only the centre's is read)
-    __shared__ float4 Y[N];     // YCoCg (+ pad): one 16-byte read per neighbour
+    constexpr int RING = N - kTaaW * kTaaH;  // 164 halo pixels
+    constexpr int KN = kTaaH / 4;            // output pixels per thread
+    __shared__ float4 Y[N];                  // YCoCg (+ pad): one 16-byte read per neighbour
     const int t = threadIdx.x;
     // Output tile of this launch (the whole image, or a multi-GPU tile whose
     // one-pixel halo lies inside the buffer region).
@@ -132,69 +144,63 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, const float* __rest
     const int bxi = gi % gridDim.x, byi = gi / gridDim.x;
 #endif
     const int x0 = P.tx0 + bxi * kTaaW, y0 = P.ty0 + byi * kTaaH;
-    // Three dependent round trips per pixel (reprojection -> previous-frame
-    // taps, and the tile) are overlapped: the reprojected positions go out
-    // first, the tile loads behind them, and the taps as soon as the
-    // positions are back -- all before the tile is tone-mapped into LDS.
-    const int tx = t & (kTaaW - 1);
-    float2 pf[kTaaH / 4];
+    const int tx = t & (kTaaW - 1), ty = t >> 6;
+    // Reprojected positions first, then the tile and its ring behind them.
+    float2 pf[KN];
 #pragma unroll
-    for (int k = 0; k < kTaaH / 4; ++k) {
-        const int x = min(x0 + tx, P.tx1 - 1), y = min(y0 + (t >> 6) + 4 * k, P.ty1 - 1);
-        pf[k] = prev_pixel[pix(P, x, y)];
+    for (int k = 0; k < KN; ++k)
+        pf[k] = prev_pixel[pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + ty + 4 * k, P.ty1 - 1))];
+    f3 v[KN + 1], al[KN + 1];
+    int hx = 0, hy = 0;  // this thread's ring pixel (t < RING), in tile + halo coordinates
+    if (t < 2 * HW) {
+        hx = t % HW;
+        hy = t < HW ? 0 : HH - 1;
+    } else {
+        hx = t < 2 * HW + kTaaH ? 0 : HW - 1;
+        hy = 1 + (t - 2 * HW) % kTaaH;
     }
-    f3 v[ITER], al[ITER];
 #pragma unroll
-    for (int k = 0; k < ITER; ++k) {
-        const int i = t + 256 * k;
-        const int x = min(max(x0 - 1 + i % HW, 0), P.width - 1), y = min(max(y0 - 1 + i / HW, 0), P.height - 1);
-        const long lin = pix(P, x, y);
+    for (int k = 0; k <= KN; ++k) {
+        const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + 4 * k + 1 : hy;
+        if (k == KN && t >= RING) break;
+        const long lin = pix(P, min(max(x0 - 1 + lx, 0), P.width - 1), min(max(y0 - 1 + ly, 0), P.height - 1));
         v[k] = ld3(src, lin);
         if (TONE) al[k] = ld3in<IN>(albedo, lin);
     }
-#ifndef BMFR_K2_EARLY_TAPS
-#define BMFR_K2_EARLY_TAPS 1
-#endif
-    f3 taps[kTaaH / 4][4];
+    f3 taps[KN][4];
     if constexpr (BMFR_K2_EARLY_TAPS) {
 #pragma unroll
-        for (int k = 0; k < kTaaH / 4; ++k) taa_load_taps(P, pf[k], prev_frame, taps[k]);
+        for (int k = 0; k < KN; ++k) taa_load_taps(P, pf[k], prev_frame, taps[k]);
     }
 #pragma unroll
-    for (int k = 0; k < ITER; ++k) {
-        const int i = t + 256 * k;
-        if (i < N) {  // clamped halo entries are never read
-            const f3 c = TONE ? tone_map(al[k], v[k]) : v[k];
-            const f3 yc = rgb_to_ycocg(c);
-            T[0][i] = c.x;
-            T[1][i] = c.y;
-            T[2][i] = c.z;
-            Y[i] = make_float4(yc.x, yc.y, yc.z, 0.f);
-        }
+    for (int k = 0; k <= KN; ++k) {
+        if (k == KN && t >= RING) break;
+        const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + 4 * k + 1 : hy;
+        v[k] = TONE ? tone_map(P, al[k], v[k]) : v[k];
+        const f3 yc = rgb_to_ycocg(v[k]);
+        Y[ly * HW + lx] = make_float4(yc.x, yc.y, yc.z, 0.f);
     }
     __syncthreads();
     if constexpr (!BMFR_K2_EARLY_TAPS) {
 #pragma unroll
-        for (int k = 0; k < kTaaH / 4; ++k) taa_load_taps(P, pf[k], prev_frame, taps[k]);
+        for (int k = 0; k < KN; ++k) taa_load_taps(P, pf[k], prev_frame, taps[k]);
     }
     // Tiles that reach the image border check every neighbour (bmfr.cl:901);
     // the others have all nine in the image.
     const bool edge = x0 == 0 || y0 == 0 || x0 + kTaaW >= P.width || y0 + kTaaH >= P.height;
 #pragma unroll
-    for (int k = 0; k < kTaaH / 4; ++k) {
-        const int ty = (t >> 6) + 4 * k;
-        const int x = x0 + tx, y = y0 + ty;
+    for (int k = 0; k < KN; ++k) {
+        const int x = x0 + tx, y = y0 + ty + 4 * k;
         if (x < P.tx1 && y < P.ty1) {
-            const int c = (ty + 1) * HW + tx + 1;
-            const f3 me{T[0][c], T[1][c], T[2][c]};
+            const int c = (ty + 4 * k + 1) * HW + tx + 1;
             f3 nb[9];
 #pragma unroll
             for (int j = 0; j < 9; ++j) {
                 const float4 q = Y[c + (j / 3 - 1) * HW + (j % 3 - 1)];
                 nb[j] = f3{q.x, q.y, q.z};
             }
-            const f3 r = edge ? taa_resolve<true>(P, x, y, me, pf[k], nb, taps[k], frame)
-                              : taa_resolve<false>(P, x, y, me, pf[k], nb, taps[k], frame);
+            const f3 r = edge ? taa_resolve<true>(P, x, y, v[k], pf[k], nb, taps[k], frame)
+                              : taa_resolve<false>(P, x, y, v[k], pf[k], nb, taps[k], frame);
             st3(result, pix(P, x, y), r);
         }
     }

@@ -36,6 +36,7 @@ struct Params {
     float position_limit_sq, normal_limit_sq;
     int half_tmp;                 // USE_HALF_PRECISION_IN_TMP_DATA
     int input_half;               // bmfr_config.input_half: frame input planes are half3
+    int library_powr;             // bmfr_config.library_powr: tone map with __ocml_powr_f32
     int fused_variant;            // 0 = default, 1 = generic-feature K1, 2 = tone map in K1, 3 = row-split K1,
                                   // 4 = tone map in K1 + stencil K2, 5 = tone map in column-split K1
                                   // + LDS K2 (A/B diagnostics)

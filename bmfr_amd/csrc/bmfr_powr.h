@@ -1,0 +1,43 @@
+// The tone map's powr(x, 0.454545f) (bmfr.cl:854), correctly rounded.
+//
+// OpenCL leaves powr's rounding to the device (up to 16 ulp), so the
+// reference fixes no bit pattern here; the CPU oracle takes the correctly
+// rounded value ((float)pow in double, oracle/bmfr_oracle.c).  This is that
+// value, computed in ~20 instructions instead of the device library's ~130
+// (the extended-precision log/exp of __ocml_powr_f32), which made the tone
+// map 55 % of K2's VALU work:
+//   x = m 2^e, m in [0.5, 1):  x^c = 2^(e c) * rc_j^-c * (1 + u)^c,
+//   u = m rc_j - 1 (exact, |u| < 2^-8), (1 + u)^c a degree-4 series,
+// all in double (relative error < 2^-45), rounded once to float.  A result
+// whose double lies within 2^10 double ulps of a float rounding midpoint
+// (about one input in 2^18) is recomputed with the device library's f64 pow.
+// tools/powr_check.hip checks every float in (0, 1) against (float)pow.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bmfr_powr_tables.h"
+
+extern "C" __device__ double __ocml_pow_f64(double, double);
+extern "C" __device__ float __ocml_powr_f32(float, float);
+
+// min(max(powr(max(0, p), 0.454545f), 0), 1) (bmfr.cl:853-855).
+__device__ __forceinline__ float gamma_clamped(float p) {
+    const bool pos = p > 0.f, below = p < 1.f;
+    const float x = pos && below ? p : 0.5f;
+    const float m = __builtin_amdgcn_frexp_mantf(x);
+    const int e = __builtin_amdgcn_frexp_expf(x);
+    const int j = (int)(__float_as_uint(m) >> (23 - BMFR_POWR_J_BITS)) & ((1 << BMFR_POWR_J_BITS) - 1);
+    const double2 rp = kPowrRP[j];
+    const double ep = kPowrE[e - BMFR_POWR_E_MIN] * rp.y;
+    const double u = __builtin_fma((double)m, rp.x, -1.0);
+    double q = __builtin_fma(BMFR_POWR_A4, u, BMFR_POWR_A3);
+    q = __builtin_fma(q, u, BMFR_POWR_A2);
+    q = __builtin_fma(q, u, BMFR_POWR_A1);
+    const double r = __builtin_fma(ep, u * q, ep);
+    float v = (float)r;
+    const uint32_t low = (uint32_t)__double_as_longlong(r) & 0x1FFFFFFFu;
+    if (__builtin_expect(low - (0x10000000u - 1024u) < 2048u, 0))
+        v = (float)__ocml_pow_f64((double)x, (double)0.454545f);
+    return pos ? (below ? v : 1.f) : 0.f;
+}

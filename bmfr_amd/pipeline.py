@@ -49,6 +49,9 @@ class BmfrConfig:
     tile_halo: int = 0
     # Frame input planes in IEEE half (half3, 6 B/px) instead of f32 (include/bmfr.h: input_half)
     input_half: int = 0
+    # Tone map powr: 0 = correctly rounded (== the CPU oracle), 1 = the device
+    # library's powr (== the reference kernel on gfx950) (include/bmfr.h: library_powr)
+    library_powr: int = 0
 
     @property
     def buffer_count(self) -> int:
@@ -74,6 +77,7 @@ class BmfrConfig:
             c.tile_x, c.tile_y, c.tile_width, c.tile_height = self.tile
             c.tile_halo = self.tile_halo
         c.input_half = self.input_half
+        c.library_powr = self.library_powr
         return c
 
     def sizes(self) -> _lib.Sizes:

@@ -99,6 +99,13 @@ typedef struct bmfr_config {
      * output equals the f32 path's on the widened planes bit for bit.
      * Canonical feature lists, fused path only (stage API: unsupported). */
     int input_half;
+    /* powr(x, 0.454545f) of the tone map (bmfr.cl:854), whose rounding
+     * OpenCL leaves to the device: 0 (default) = correctly rounded, equal to
+     * the CPU oracle's (float)pow for every input, ~20 instructions;
+     * 1 = the device library's __ocml_powr_f32, i.e. what the reference
+     * kernel compiled for gfx950 computes (one in four results 1 ulp from
+     * the correctly rounded one), ~130 instructions. */
+    int library_powr;
 } bmfr_config;
 
 /* Sizes derived from a config (bmfr.cpp:104-118, 316-343). */

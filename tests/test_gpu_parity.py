@@ -9,11 +9,13 @@ on the synthetic sequence, every inter-stage buffer recorded:
   HIP    libbmfr: the five stage kernels (StagePipeline) and the fused frame
          path (Denoiser)
 
-Bars: HIP stages == REF(strict) bit for bit on every buffer; fused ==
-stages bit for bit; ORACLE == REF(strict) bit for bit except tone/result
-(powr: GPU library vs correctly rounded CPU pow, |diff| <= 2 ulp-ish); HIP
-vs REF(default build, contraction on) within relative L2 1e-4 (fp32 tmp)
-on the TAA output.
+Bars: HIP stages (library_powr = 1: the device library's powr, as the
+reference kernel calls it) == REF(strict) bit for bit on every buffer; HIP
+stages (default: correctly rounded powr) == ORACLE bit for bit on every
+buffer; fused == stages bit for bit in both modes; ORACLE == REF(strict) bit
+for bit except tone/result (powr: GPU library vs correctly rounded CPU pow,
+|diff| <= 2 ulp-ish); HIP vs REF(default build, contraction on) within
+relative L2 1e-4 (fp32 tmp) on the TAA output.
 """
 from __future__ import annotations
 
@@ -36,11 +38,11 @@ def _dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-def bmfr_cfg(rc) -> bmfr_amd.BmfrConfig:
+def bmfr_cfg(rc, library_powr=0) -> bmfr_amd.BmfrConfig:
     return bmfr_amd.BmfrConfig(image_width=rc.width, image_height=rc.height, not_scaled=rc.not_scaled,
                                scaled=rc.scaled, use_half_precision_in_tmp_data=rc.half_tmp,
                                position_limit_squared=rc.position_limit_squared,
-                               normal_limit_squared=rc.normal_limit_squared)
+                               normal_limit_squared=rc.normal_limit_squared, library_powr=library_powr)
 
 
 _cache = {}
@@ -57,22 +59,29 @@ def ref_frames(name, mode="strict"):
     return _cache[key]
 
 
-def stage_frames(name):
-    key = (name, "stages")
+def stage_frames(name, library_powr=0):
+    key = (name, "stages", library_powr)
     if key not in _cache:
         rc = REF_CONFIGS[name]
-        _cache[key] = run_loop(bmfr_amd.StagePipeline(bmfr_cfg(rc)), rc, rc.frames, to_device=_dev,
+        _cache[key] = run_loop(bmfr_amd.StagePipeline(bmfr_cfg(rc, library_powr)), rc, rc.frames, to_device=_dev,
                                sync=torch.cuda.synchronize)
+    return _cache[key]
+
+
+def oracle_frames(name):
+    key = (name, "oracle")
+    if key not in _cache:
+        rc = REF_CONFIGS[name]
+        cfg = pyoracle.make_cfg(rc.width, rc.height, rc.not_scaled, rc.scaled, rc.half_tmp)
+        _cache[key] = run_loop(pyoracle.OracleLoop(cfg), rc, rc.frames)
     return _cache[key]
 
 
 @pytest.mark.parametrize("name", CONFIGS)
 def test_oracle_matches_reference_kernels(name, gpu):
     """Pins the CPU oracle to the reference itself."""
-    rc = REF_CONFIGS[name]
     ref = ref_frames(name)
-    cfg = pyoracle.make_cfg(rc.width, rc.height, rc.not_scaled, rc.scaled, rc.half_tmp)
-    orc = run_loop(pyoracle.OracleLoop(cfg), rc, rc.frames)
+    orc = oracle_frames(name)
     compare_exact(orc, ref, EXACT_KEYS, f"oracle vs reference[{name}]")
     for f, (o, r) in enumerate(zip(orc, ref)):
         for k in POWR_KEYS:
@@ -82,14 +91,23 @@ def test_oracle_matches_reference_kernels(name, gpu):
 
 @pytest.mark.parametrize("name", CONFIGS)
 def test_stage_kernels_match_reference_bitwise(name, gpu):
-    compare_exact(stage_frames(name), ref_frames(name), ALL_KEYS, f"HIP stages vs reference[{name}]")
+    """library_powr: the reference kernel's own powr, so every buffer is pinned."""
+    compare_exact(stage_frames(name, 1), ref_frames(name), ALL_KEYS, f"HIP stages vs reference[{name}]")
 
 
 @pytest.mark.parametrize("name", CONFIGS)
-def test_fused_frame_matches_stages_bitwise(name, gpu):
+def test_stage_kernels_match_oracle_bitwise(name, gpu):
+    """Default (correctly rounded powr): every buffer, tone map and TAA output
+    included, equals the CPU oracle's."""
+    compare_exact(stage_frames(name), oracle_frames(name), ALL_KEYS, f"HIP stages vs oracle[{name}]")
+
+
+@pytest.mark.parametrize("library_powr", [0, 1])
+@pytest.mark.parametrize("name", CONFIGS)
+def test_fused_frame_matches_stages_bitwise(name, library_powr, gpu):
     rc = REF_CONFIGS[name]
-    st = stage_frames(name)
-    den = bmfr_amd.Denoiser(bmfr_cfg(rc))
+    st = stage_frames(name, library_powr)
+    den = bmfr_amd.Denoiser(bmfr_cfg(rc, library_powr))
     n = rc.width * rc.height
     for f in range(rc.frames):
         from seq_util import camera, frame_inputs
