@@ -616,7 +616,8 @@ __device__ __forceinline__ f3 blend_filtered(const Params& P, f3 filtered, float
 // Albedo remodulation + 1/2.2 gamma + clamp (bmfr.cl:851-856), with powr
 // correctly rounded (bmfr_powr.h: equal to the oracle's for every input) or,
 // with library_powr, the device library's as the reference kernel calls it.
-__device__ __forceinline__ f3 tone_map(const Params& P, f3 albedo, f3 a) {
+__device__ __forceinline__ f3 tone_map(const Params& P, f3 albedo, f3 a, const double* tE = kPowrE,
+                                       const double2* tRP = kPowrRP) {
     const f3 p{albedo.x * a.x, albedo.y * a.y, albedo.z * a.z};
     if (P.library_powr) {
         const float g = 0.454545f;
@@ -624,7 +625,7 @@ __device__ __forceinline__ f3 tone_map(const Params& P, f3 albedo, f3 a) {
                   fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, p.y), g), 0.f), 1.f),
                   fminf(fmaxf(__ocml_powr_f32(fmaxf(0.f, p.z), g), 0.f), 1.f)};
     }
-    return f3{gamma_clamped(p.x), gamma_clamped(p.y), gamma_clamped(p.z)};
+    return f3{gamma_clamped(p.x, tE, tRP), gamma_clamped(p.y, tE, tRP), gamma_clamped(p.z, tE, tRP)};
 }
 
 // The four bilinear taps of the previous TAA output at reprojected position

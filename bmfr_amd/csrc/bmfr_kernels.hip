@@ -121,7 +121,7 @@ constexpr int kTaaW = 64, kTaaH = BMFR_K2_H;
 #define BMFR_K2_WAVES 1
 #endif
 #ifndef BMFR_K2_EARLY_TAPS  // previous-frame taps loaded before the tone map
-#define BMFR_K2_EARLY_TAPS 0
+#define BMFR_K2_EARLY_TAPS 1
 #endif
 template <bool TONE, class IN>
 __global__ __launch_bounds__(256, BMFR_K2_WAVES) void k_fused_taa(Params P, const float* __restrict__ src,
@@ -134,7 +134,10 @@ __global__ __launch_bounds__(256, BMFR_K2_WAVES) void k_fused_taa(Params P, cons
     constexpr int RING = N - kTaaW * kTaaH;  // 164 halo pixels
     constexpr int KN = kTaaH / 4;            // output pixels per thread
     __shared__ float4 Y[N];                  // YCoCg (+ pad): one 16-byte read per neighbour
+    __shared__ double sE[TONE ? kPowrENum : 1];
+    __shared__ double2 sRP[TONE ? kPowrRPNum : 1];
     const int t = threadIdx.x;
+    if constexpr (TONE) bmfr_powr_tables_to_lds<256>(sE, sRP, t);
     // Output tile of this launch (the whole image, or a multi-GPU tile whose
     // one-pixel halo lies inside the buffer region).
 #ifdef BMFR_NO_XCD_SWIZZLE
@@ -172,11 +175,12 @@ __global__ __launch_bounds__(256, BMFR_K2_WAVES) void k_fused_taa(Params P, cons
 #pragma unroll
         for (int k = 0; k < KN; ++k) taa_load_taps(P, pf[k], prev_frame, taps[k]);
     }
+    if constexpr (TONE) __syncthreads();  // the powr tables are in LDS
 #pragma unroll
     for (int k = 0; k <= KN; ++k) {
         if (k == KN && t >= RING) break;
         const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + 4 * k + 1 : hy;
-        v[k] = TONE ? tone_map(P, al[k], v[k]) : v[k];
+        v[k] = TONE ? tone_map(P, al[k], v[k], sE, sRP) : v[k];
         const f3 yc = rgb_to_ycocg(v[k]);
         Y[ly * HW + lx] = make_float4(yc.x, yc.y, yc.z, 0.f);
     }

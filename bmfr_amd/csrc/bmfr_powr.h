@@ -21,15 +21,18 @@
 extern "C" __device__ double __ocml_pow_f64(double, double);
 extern "C" __device__ float __ocml_powr_f32(float, float);
 
-// min(max(powr(max(0, p), 0.454545f), 0), 1) (bmfr.cl:853-855).
-__device__ __forceinline__ float gamma_clamped(float p) {
+// min(max(powr(max(0, p), 0.454545f), 0), 1) (bmfr.cl:853-855), with the
+// tables read from `tE` / `tRP`: kPowrE / kPowrRP in global memory, or a
+// work-group's copy in LDS (bmfr_powr_tables_to_lds), which keeps the two
+// lookups per channel off the vector-memory path.
+__device__ __forceinline__ float gamma_clamped(float p, const double* tE = kPowrE, const double2* tRP = kPowrRP) {
     const bool pos = p > 0.f, below = p < 1.f;
     const float x = pos && below ? p : 0.5f;
     const float m = __builtin_amdgcn_frexp_mantf(x);
     const int e = __builtin_amdgcn_frexp_expf(x);
     const int j = (int)(__float_as_uint(m) >> (23 - BMFR_POWR_J_BITS)) & ((1 << BMFR_POWR_J_BITS) - 1);
-    const double2 rp = kPowrRP[j];
-    const double ep = kPowrE[e - BMFR_POWR_E_MIN] * rp.y;
+    const double2 rp = tRP[j];
+    const double ep = tE[e - BMFR_POWR_E_MIN] * rp.y;
     const double u = __builtin_fma((double)m, rp.x, -1.0);
     double q = __builtin_fma(BMFR_POWR_A4, u, BMFR_POWR_A3);
     q = __builtin_fma(q, u, BMFR_POWR_A2);
@@ -40,4 +43,14 @@ __device__ __forceinline__ float gamma_clamped(float p) {
     if (__builtin_expect(low - (0x10000000u - 1024u) < 2048u, 0))
         v = (float)__ocml_pow_f64((double)x, (double)0.454545f);
     return pos ? (below ? v : 1.f) : 0.f;
+}
+
+constexpr int kPowrENum = sizeof(kPowrE) / sizeof(double), kPowrRPNum = sizeof(kPowrRP) / sizeof(double2);
+
+// Copy the tables to LDS (all threads of the work-group; a barrier must
+// follow before gamma_clamped reads them).
+template <int NT>
+__device__ __forceinline__ void bmfr_powr_tables_to_lds(double* sE, double2* sRP, int t) {
+    for (int i = t; i < kPowrRPNum; i += NT) sRP[i] = kPowrRP[i];
+    for (int i = t; i < kPowrENum; i += NT) sE[i] = kPowrE[i];
 }
