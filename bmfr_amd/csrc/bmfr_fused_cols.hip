@@ -122,6 +122,57 @@ __device__ __forceinline__ float sub_h(h2 h, float q) {
 // With the fast path, the division is a Markstein step on the shared
 // reciprocal (exact for these operand ranges, tests/test_markstein.py);
 // non-finite or extreme operands take IEEE division (uniform branch).
+#ifndef BMFR_PK_UPDATE
+#define BMFR_PK_UPDATE 1  // column update on packed f32 pairs (v_pk_add/mul/fma_f32)
+#endif
+#if BMFR_PK_UPDATE
+typedef float f2v __attribute__((ext_vector_type(2)));
+// The same per-element operations as below, two rows per instruction: the
+// dot's four partial chains run as two packed pairs (chain m sums rows
+// j = m + 4 si in order si = 0..3, so rows 4si, 4si+1 of one step feed
+// chains 0, 1 together), and the quotients as packed Markstein steps.  Every
+// lane of a packed op rounds like the scalar op, so the results are the
+// scalar path's bit for bit.
+template <int c>
+__device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
+                                              int l) {
+    f2v s01 = {0.f, 0.f}, s23 = {0.f, 0.f};
+#pragma unroll
+    for (int si = 0; si < 4; ++si) {
+        f2v p01 = {mul_h<0>(a[2 * si], u[4 * si]), mul_h<1>(a[2 * si], u[4 * si + 1])};
+        const f2v p23 = {mul_h<0>(a[2 * si + 1], u[4 * si + 2]), mul_h<1>(a[2 * si + 1], u[4 * si + 3])};
+        if (si == 0) p01.x = l >= c ? p01.x : 0.f;  // rows above the pivot: skipped
+        s01 = s01 + p01;
+        s23 = s23 + p23;
+    }
+    const float p[4] = {s01.x, s01.y, s23.x, s23.y};
+    const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);  // (2u) dot == u (2 dot): same real product, one rounding
+    f2v q[kSlots / 2];
+    if (fabsf(c2) < 0x1p100f && ulen2 >= 0x1p-100f && ulen2 < 0x1p100f) {
+        const f2v vb = {ulen2, ulen2}, vy = {recip, recip};
+#pragma unroll
+        for (int k = 0; k < kSlots / 2; ++k) {
+            const f2v av = f2v{u[2 * k], u[2 * k + 1]} * c2;
+            const f2v q0 = av * vy;
+            const f2v r = __builtin_elementwise_fma(-q0, vb, av);
+            q[k] = __builtin_elementwise_fma(r, vy, q0);
+        }
+    } else {
+        float c2s = c2;  // opaque: keeps the products inside this (cold) branch
+        asm volatile("" : "+v"(c2s));
+#pragma unroll
+        for (int j = 0; j < kSlots; ++j) {
+            q[j >> 1][j & 1] = (u[j] * c2s) / ulen2;
+            __builtin_amdgcn_sched_barrier(0);  // never taken in practice: keep it narrow
+        }
+    }
+    q[0].x = l >= c ? q[0].x : 0.f;  // x - (+0) == x: rows above the pivot keep their value
+#pragma unroll
+    for (int k = 0; k < kSlots / 2; ++k)
+        a[k] = __builtin_convertvector((f2v{sub_h<0>(a[k], q[k].x), sub_h<1>(a[k], q[k].y)}), h2);
+    __builtin_amdgcn_sched_barrier(0);  // one column in flight: bounds the register footprint
+}
+#else
 template <int c>
 __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
                                               int l) {
@@ -160,6 +211,8 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
     }
     __builtin_amdgcn_sched_barrier(0);  // one column in flight: bounds the register footprint
 }
+
+#endif
 
 // Step 0: column 0 is FEATURE_BUFFERS[0] = 1.f, so u = (1 - 32, 1, 1, ...),
 // |u|^2 = 1984 and u*x = x exactly (see k_fused's qr_column<0>).  Noise is
