@@ -20,10 +20,10 @@ DESIGN.md "Multi-GPU").  Default --scaling weak: every rank's tile is
 strong splits one --width x --height frame.  Timing: barrier + synchronize
 around K frames (exchange included), max over ranks.
 
-The timed frames run without per-kernel events; `kernel_ms`,
-`device_ms_per_frame` and the roofline's K1 time come from HIP events over
-the next (up to 10) frames of the same sequence, on the stream the kernels
-run on.
+`kernel_ms`, `device_ms_per_frame` and the roofline's K1 time come from HIP
+events around the kernels of every 10th timed frame (libbmfr's profiling
+stride), recorded on the stream the kernels run on; the other timed frames
+run without events.
 
 Extra JSON fields: `roofline` for the dominant kernel (K1); `cpu_baseline` = the CPU oracle
 (oracle/liboracle.so, OpenMP) on a bounded sample of the same sequence.
@@ -67,7 +67,7 @@ def frame_bytes_per_px(s: int) -> int:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
@@ -135,6 +135,9 @@ def pmc_traffic(workload: str):
     return d.get(workload, {}).get("hbm_bytes_per_launch")
 
 
+PROF_STRIDE = 10  # timed frames between two recorded with per-kernel events
+
+
 def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, per_frame=False):
     """Denoise frames 0..warmup+steps-1 of the synthetic W x H sequence (this
     rank's tile of it); time the last `steps` frames.  Returns the timings,
@@ -147,10 +150,10 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     local = dev.index
     den = bmfr_amd.Denoiser(cfg, device=local)
     region = den.region
-    # Timed frames run without the per-kernel events; the next `prof` frames
-    # of the sequence are run with them for the kernel breakdown.
-    prof = max(1, min(steps, 10))
-    nfr = warmup + steps + prof
+    # Per-kernel HIP events are recorded on every PROF_STRIDE-th frame of the
+    # timed region (libbmfr's profiling stride), so the kernel breakdown and
+    # the roofline come from the timed frames at a small cost to the rest.
+    nfr = warmup + steps
     seed = a.seed
 
     # Render every frame's region into HBM up front (untimed).
@@ -205,6 +208,8 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
 
     if warmup:
         run_range(0, warmup)
+    stride = PROF_STRIDE if steps >= PROF_STRIDE else 1
+    den.set_profiling(True, capacity=steps, stride=stride)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -219,10 +224,8 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    den.set_profiling(True, capacity=prof)
-    run_range(warmup + steps, nfr)
-    torch.cuda.synchronize()
     kprof = den.profile()
+    den.set_profiling(False)
 
     # Quality: PSNR of this rank's tile of the last output against the clean render.
     clean = bmfr_amd.synth_region_device(W, H, region, nfr - 1, seed=seed, device=local, clean=True)["clean"]

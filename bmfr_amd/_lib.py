@@ -106,6 +106,7 @@ SIGNATURES = {
     "bmfr_output": (_P, [_P]),
     "bmfr_state": (_I, [_P, _I, C.POINTER(StateView)]),
     "bmfr_set_profiling": (_I, [_P, _I, _I]),
+    "bmfr_set_profiling_stride": (_I, [_P, _I]),
     "bmfr_get_profile": (_I, [_P, C.POINTER(FrameProfile), _I, C.POINTER(_I)]),
     "bmfr_synth_camera": (None, [_I, _I, _I, _F16, _F2]),
     "bmfr_debug_stamps": (_I, [_P, _P, C.c_size_t]),  # include/bmfr_debug.h

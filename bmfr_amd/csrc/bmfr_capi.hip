@@ -41,6 +41,7 @@ struct bmfr_ctx {
     int pending_frame = -1;
     // Profiling ring: 3 events per frame (before K1, after K1, after K2).
     int prof_capacity = 0;
+    int prof_stride = 1;  // record frames whose number is a multiple of this
     long prof_count = 0;
     hipEvent_t* prof_events = nullptr;
     int* prof_frames = nullptr;
@@ -527,7 +528,7 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
     const Params P = frame_params(c, frame_number);
     if (part != 2 && !bmfr::fused_supported(P)) return BMFR_ERROR_UNSUPPORTED;
     hipEvent_t* ev = nullptr;
-    if (c->prof_capacity > 0) {
+    if (c->prof_capacity > 0 && frame_number % c->prof_stride == 0) {
         const long n = part == 1 ? c->prof_count - 1 : c->prof_count;
         ev = c->prof_events + 3 * (int)(n % c->prof_capacity);
     }
@@ -630,7 +631,7 @@ bmfr_status bmfr_process_sequence(bmfr_ctx* c, void* stream, int count, const bm
                                        f, cur);
         const Params P = frame_params(c, f);
         hipEvent_t* ev = nullptr;
-        if (c->prof_capacity > 0) {
+        if (c->prof_capacity > 0 && f % c->prof_stride == 0) {
             const int slot = (int)(c->prof_count % c->prof_capacity);
             ev = c->prof_events + 3 * slot;
             c->prof_frames[slot] = f;
@@ -700,6 +701,12 @@ bmfr_status bmfr_halo_copy(bmfr_ctx* c, void* stream, const int* rects, int n, v
     if (bytes) *bytes = (size_t)off;
     if (!buffer) return BMFR_OK;
     return hip_status(bmfr::launch_halo_copy(a, as_stream(stream), buffer, unpack));
+}
+
+bmfr_status bmfr_set_profiling_stride(bmfr_ctx* c, int stride) {
+    if (!c || stride <= 0) return BMFR_ERROR_INVALID_ARGUMENT;
+    c->prof_stride = stride;
+    return BMFR_OK;
 }
 
 bmfr_status bmfr_set_profiling(bmfr_ctx* c, int enable, int capacity) {

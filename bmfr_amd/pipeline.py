@@ -254,7 +254,9 @@ class Denoiser(_Context):
         self._call("bmfr_process_frame_border", noisy, normals, positions, albedo, prev_vp, jitter, frame,
                    prev_normals, prev_positions, stream, True)
 
-    def set_profiling(self, enable: bool, capacity: int = 4096) -> None:
+    def set_profiling(self, enable: bool, capacity: int = 4096, stride: int = 1) -> None:
+        """stride: record only frames whose number is a multiple of it."""
+        check(self.lib.bmfr_set_profiling_stride(self.handle, stride), "bmfr_set_profiling_stride")
         check(self.lib.bmfr_set_profiling(self.handle, int(enable), capacity), "bmfr_set_profiling")
 
     def profile(self):

@@ -275,6 +275,9 @@ typedef struct bmfr_frame_profile {
     float total_ms;       /* start of K1 -> end of K2 (bmfr.cpp:497-502) */
 } bmfr_frame_profile;
 bmfr_status bmfr_set_profiling(bmfr_ctx *ctx, int enable, int capacity);
+/* Record only frames whose frame_number is a multiple of `stride` (default
+ * 1): per-kernel timings sampled inside a long timed run at a small cost. */
+bmfr_status bmfr_set_profiling_stride(bmfr_ctx *ctx, int stride);
 bmfr_status bmfr_get_profile(bmfr_ctx *ctx, bmfr_frame_profile *out, int max_frames, int *count);
 
 /* ---- Synthetic scene (stands in for the external EXR dataset) ---- */

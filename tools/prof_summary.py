@@ -6,6 +6,8 @@
   prof_summary.py calib <dir> <counter> <bytes>   counter / true bytes per calibration kernel
   prof_summary.py traffic <fetch_dir> <write_dir> <workload> <pixels> <alg_bytes_per_px>
                                        -> profiles/pmc_k1.json entry (HBM bytes per K1 launch)
+  prof_summary.py sq <dir> [<dir> ...] -> profiles/r01_sq_counters.json (K1 / K2 per-launch
+                                       means of every counter in the passes, plus derived rates)
 
 FETCH_SIZE / WRITE_SIZE are KB per dispatch (rocprofv3 derived counters).
 MI355X_MICROARCH.md (HBM): on gfx950 FETCH_SIZE reads half the bytes of a
@@ -37,10 +39,18 @@ def short(name):
 
 def stats(d):
     rows = list(csv.DictReader(open(find(d, "*kernel_stats.csv"))))
-    out = ["| kernel | calls | total ms | avg us | min us | max us | % |", "|---|---|---|---|---|---|---|"]
+    med = {}  # median duration per kernel from the kernel trace (steady state, without the cold first frames)
+    hits = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if hits:
+        for r in csv.DictReader(open(hits[0])):
+            med.setdefault(r["Kernel_Name"], []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    out = ["| kernel | calls | total ms | avg us | median us | min us | max us | % |",
+           "|---|---|---|---|---|---|---|---|"]
     for r in rows:
+        m = med.get(r["Name"])
+        ms = f"{statistics.median(m) / 1e3:.1f}" if m else "-"
         out.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
-                   f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['MinNs']) / 1e3:.1f} | "
+                   f"{float(r['AverageNs']) / 1e3:.1f} | {ms} | {float(r['MinNs']) / 1e3:.1f} | "
                    f"{float(r['MaxNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} |")
     return "\n".join(out)
 
@@ -55,6 +65,31 @@ def pmc(d, counter):
     return {k: statistics.mean(v) for k, v in per.items()}
 
 
+KERNELS = {"K1 k_fused_cols": "k_fused_cols<4, 6, float, false>", "K2 k_fused_taa": "k_fused_taa<true, float>"}
+
+
+def sq(dirs):
+    out = {}
+    for key, name in KERNELS.items():
+        c = {}
+        for d in dirs:
+            for r in csv.DictReader(open(find(d, "*counter_collection.csv"))):
+                if short(r["Kernel_Name"]).startswith(name):
+                    c.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        e = {k: round(statistics.mean(v), 3) for k, v in sorted(c.items())}
+        if "SQ_INSTS_VALU" in e and "SQ_WAVES" in e:
+            e["valu_instr_per_wave"] = round(e["SQ_INSTS_VALU"] / e["SQ_WAVES"], 3)
+            e["valu_instr_per_simd"] = round(e["SQ_INSTS_VALU"] / 1024, 3)  # 256 CUs x 4 SIMDs
+        if "SQ_WAIT_ANY" in e and "SQ_WAVE_CYCLES" in e:
+            e["wait_any_frac_of_wave_cycles"] = round(e["SQ_WAIT_ANY"] / e["SQ_WAVE_CYCLES"], 3)
+        if "GRBM_GUI_ACTIVE" in e:
+            e["kernel_cycles_per_xcd"] = round(e["GRBM_GUI_ACTIVE"] / 8, 3)
+            if "TA_BUSY_avr" in e:
+                e["ta_busy_frac"] = round(e["TA_BUSY_avr"] / e["kernel_cycles_per_xcd"], 3)
+        out[key] = e
+    return out
+
+
 def main():
     cmd = sys.argv[1]
     if cmd == "stats":
@@ -65,6 +100,12 @@ def main():
         true_kb = int(sys.argv[4]) / 1024
         for k, v in pmc(sys.argv[2], sys.argv[3]).items():
             print(f"{k:40s} {sys.argv[3]} {v:12.0f} KB  counted/true {v / true_kb:.3f}")
+    elif cmd == "sq":
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                            "r01_sq_counters.json")
+        d = sq(sys.argv[2:])
+        json.dump(d, open(path, "w"), indent=1)
+        print(json.dumps(d, indent=1))
     elif cmd == "traffic":
         fetch_dir, write_dir, workload, px, alg = sys.argv[2:7]
         k1 = os.environ.get("K1_NAME", "k_fused_cols<4, 6")
