@@ -34,6 +34,12 @@ namespace cols {
 
 constexpr int kThreads = 256;
 constexpr int kSlots = 16;    // rows per lane per column (row = lane + 64 j)
+#ifndef BMFR_PK_P3
+#define BMFR_PK_P3 1  // weighted sum over packed item pairs
+#endif
+#ifndef BMFR_M_SWIZZLE
+#define BMFR_M_SWIZZLE 1  // design matrix row slots XOR-swizzled in LDS (conflict-free phase-1 stores)
+#endif
 constexpr int kUStride = 20;  // floats per lane in a u buffer: 16 + 4 (conflict-free 16-byte reads)
 
 #ifndef BMFR_PARK_GLOBAL
@@ -122,11 +128,11 @@ __device__ __forceinline__ float sub_h(h2 h, float q) {
 // With the fast path, the division is a Markstein step on the shared
 // reciprocal (exact for these operand ranges, tests/test_markstein.py);
 // non-finite or extreme operands take IEEE division (uniform branch).
+typedef float f2v __attribute__((ext_vector_type(2)));
 #ifndef BMFR_PK_UPDATE
 #define BMFR_PK_UPDATE 1  // column update on packed f32 pairs (v_pk_add/mul/fma_f32)
 #endif
 #if BMFR_PK_UPDATE
-typedef float f2v __attribute__((ext_vector_type(2)));
 // The same per-element operations as below, two rows per instruction: the
 // dot's four partial chains run as two packed pairs (chain m sums rows
 // j = m + 4 si in order si = 0..3, so rows 4si, 4si+1 of one step feed
@@ -393,11 +399,19 @@ struct WaveFit {
         sfor<NSL>([&](auto K) {
             constexpr int c = W + 4 * decltype(K)::value;
             if constexpr (owns(c)) {
+#if BMFR_M_SWIZZLE
+                // pair p of lane l's row slot sits at dword p ^ ((l >> 2) & 7) (see phase 1)
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(&L.M[c - 1][l * kSlots]);
+                const int q = (l >> 2) & 7;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) a[c >> 2][i] = __builtin_bit_cast(h2, src[i ^ q]);
+#else
                 const uint4* src = reinterpret_cast<const uint4*>(&L.M[c - 1][l * kSlots]);
                 const uint4 lo = src[0], hi = src[1];
                 const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #pragma unroll
                 for (int i = 0; i < 8; ++i) a[c >> 2][i] = __builtin_bit_cast(h2, w[i]);
+#endif
             }
         });
         k1_barrier();  // the u buffers alias M
@@ -479,7 +493,7 @@ __device__ __forceinline__ void back_substitute(Lds<B>& L, int t) {
 }
 
 #ifndef BMFR_COLS_WAVES
-#define BMFR_COLS_WAVES 1  // minimum waves per SIMD requested from the register allocator
+#define BMFR_COLS_WAVES 4  // minimum waves per SIMD requested from the register allocator (128 VGPRs: 4 WGs/CU)
 #endif
 template <int NS, int FS, class IN, bool TONE>
 __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params P, NoisyInputs in, Camera cam, int frame,
@@ -514,6 +528,9 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
     const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
 
     // ---- accumulate_noisy_data (bmfr.cl:310-484), rows l + 64 (4w + i) ----
+#if defined(BMFR_P1_B16) && BMFR_M_SWIZZLE
+#error "BMFR_P1_B16 stores halves unswizzled: build it with -DBMFR_M_SWIZZLE=0"
+#endif
     h2 pk[B];  // features of an item pair, packed for one 4-byte LDS store per column
     uint32_t spps = 0;   // per item i, bits 8i..8i+7: its new spp
     uint32_t ibits = 0;  // per item i, bit i: owner; bit 4 + i: accepted taps with weight > 0
@@ -564,10 +581,11 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
             }
 #ifndef BMFR_P1_B16
             if (i & 1) {  // rows j = 4w + i - 1, 4w + i: adjacent halves of lane l's row slot
+                // (pair 2w + i/2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)
+                const int pair = BMFR_M_SWIZZLE ? (2 * w + i / 2) ^ ((l >> 2) & 7) : 2 * w + i / 2;
 #pragma unroll
                 for (int f = 1; f < B; ++f)
-                    *reinterpret_cast<uint32_t*>(&L.M[f - 1][l * kSlots + 4 * w + i - 1]) =
-                        __builtin_bit_cast(uint32_t, pk[f]);
+                    *reinterpret_cast<uint32_t*>(&L.M[f - 1][l * kSlots + 2 * pair]) = __builtin_bit_cast(uint32_t, pk[f]);
             }
 #endif
 #ifdef BMFR_P1_SERIAL
@@ -625,6 +643,43 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
     // Features outer, items inner: each weight / min-max is live for one
     // feature only.  Every item still accumulates in feature order.
     f3 c[4];
+#if BMFR_PK_P3
+    // Items (0, 1) and (2, 3) as packed f32 pairs: every lane rounds as the
+    // scalar sequence below.
+    f2v cp[2][3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+        for (int ch = 0; ch < 3; ++ch) cp[h][ch] = f2v{0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < B - 3; ++f) {
+        const f2v wv[3] = {f2v{L.weights[3 * f], L.weights[3 * f]}, f2v{L.weights[3 * f + 1], L.weights[3 * f + 1]},
+                           f2v{L.weights[3 * f + 2], L.weights[3 * f + 2]}};
+        float bmin = 0.f, d = 0.f, rcp = 0.f;
+        if (f >= NS) {
+            bmin = L.mm[3 * (f - NS)];
+            d = L.mm[3 * (f - NS) + 1] - bmin;
+            rcp = L.mm[3 * (f - NS) + 2];
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            f2v v = {feature_value(f, nrm[2 * h], wp[2 * h]), feature_value(f, nrm[2 * h + 1], wp[2 * h + 1])};
+            if (f >= NS) {
+                v = v - f2v{bmin, bmin};
+                if (fabsf(d) > 1.0f) {
+                    const f2v q0 = v * f2v{rcp, rcp};
+                    const f2v r = __builtin_elementwise_fma(-q0, f2v{d, d}, v);
+                    v = __builtin_elementwise_fma(r, f2v{rcp, rcp}, q0);
+                }
+            }
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) cp[h][ch] = cp[h][ch] + wv[ch] * v;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one feature's weights live at a time
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+        for (int k = 0; k < 2; ++k) c[2 * h + k] = f3{cp[h][0][k], cp[h][1][k], cp[h][2][k]};
+#else
 #pragma unroll
     for (int i = 0; i < 4; ++i) c[i] = f3{0.f, 0.f, 0.f};
 #pragma unroll
@@ -649,6 +704,7 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
         }
         __builtin_amdgcn_sched_barrier(0);  // one feature's weights live at a time
     }
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (ibits & (1u << i)) {
