@@ -34,6 +34,9 @@ namespace cols {
 
 constexpr int kThreads = 256;
 constexpr int kSlots = 16;    // rows per lane per column (row = lane + 64 j)
+#ifndef BMFR_STAGGER
+#define BMFR_STAGGER 24000  // cycles; 0 = off (+1.3 % K1 throughput measured at 16-24K)
+#endif
 #ifndef BMFR_PK_P3
 #define BMFR_PK_P3 1  // weighted sum over packed item pairs
 #endif
@@ -523,6 +526,15 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 #define BMFR_STAMP(k) (void)stamps
 #endif
     BMFR_STAMP(0);
+#if BMFR_STAGGER
+    // First round of work-groups: start the k-th group of 256 k * BMFR_STAGGER
+    // cycles late, so the four work-groups sharing a CU do not run their
+    // memory-bound phase 1 and VALU-bound fit in lockstep.
+    if (blockIdx.x < 4 * 256) {
+        const int n = ((int)(blockIdx.x >> 8) & 3) * (BMFR_STAGGER / 8000);
+        for (int s = 0; s < n; ++s) __builtin_amdgcn_s_sleep(125);
+    }
+#endif
     int bx, by;
     k1_block(P, g, bx, by);
     const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
