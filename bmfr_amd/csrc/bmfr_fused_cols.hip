@@ -530,7 +530,7 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
     // First round of work-groups: start the k-th group of 256 k * BMFR_STAGGER
     // cycles late, so the four work-groups sharing a CU do not run their
     // memory-bound phase 1 and VALU-bound fit in lockstep.
-    if (blockIdx.x < 4 * 256) {
+    if (blockIdx.x < 4 * 256 && gridDim.x >= 8 * 256) {  // large launches only (not a tile's border ring)
         const int n = ((int)(blockIdx.x >> 8) & 3) * (BMFR_STAGGER / 8000);
         for (int s = 0; s < n; ++s) __builtin_amdgcn_s_sleep(125);
     }
