@@ -608,6 +608,52 @@ bmfr_status bmfr_process_sequence(bmfr_ctx* c, void* stream, int count, const bm
         if (first_frame + i > 0 && (!x.prev_normals || !x.prev_positions)) return BMFR_ERROR_INVALID_ARGUMENT;
     }
     hipError_t e = hipSuccess;
+    const char* mode = std::getenv("BMFR_SEQUENCE");  // "streams": the two-stream schedule below
+    if (bmfr::seq_fused_supported(c->P) && !(mode && std::strcmp(mode, "streams") == 0)) {
+        // One launch per frame on `stream`: K1 of frame f with K2 of frame
+        // f - 1 in its tail (k_fused_cols_taa), then K2 of the last frame.
+        // K1 of f overwrites the state slot of f - 2, whose last reader (K2
+        // of f - 2) ran in the previous launch.
+        bmfr::FusedArgs prevA{};
+        Params prevP{};
+        bool pending = false;
+        for (int i = 0; i <= count; ++i) {
+            const int f = first_frame + i;
+            bmfr::FusedArgs A{};
+            Params P{};
+            int cur = c->cur;
+            if (i < count) {
+                cur = c->has_frame ? 1 - c->cur : 0;
+                A = frame_args(c, &in[i], prev_frame_camera_matrices + 16 * i, pixel_offsets + 2 * i, f, cur);
+                P = frame_params(c, f);
+                if ((e = noise_for_frame(c, P, s, f, &A.noise_table)) != hipSuccess) return hip_status(e);
+            }
+            hipEvent_t* ev = nullptr;
+            if (i < count && c->prof_capacity > 0 && f % c->prof_stride == 0) {
+                const int slot = (int)(c->prof_count % c->prof_capacity);
+                ev = c->prof_events + 3 * slot;
+                c->prof_frames[slot] = f;
+                ++c->prof_count;
+            }
+            if (ev) (void)hipEventRecord(ev[0], s);
+            e = bmfr::launch_fused_k1_taa(P, s, i < count ? &A : nullptr, prevP, pending ? &prevA : nullptr);
+            if (ev) {  // K1 of f and K2 of f - 1 share the launch: all of it is reported as K1
+                (void)hipEventRecord(ev[1], s);
+                (void)hipEventRecord(ev[2], s);
+            }
+            if (e == hipSuccess && pending && outputs && outputs[i - 1])
+                e = hipMemcpyAsync(outputs[i - 1], prevA.result_out, out_bytes, hipMemcpyDefault, s);
+            if (e != hipSuccess) return hip_status(e);
+            if (i < count) {
+                prevA = A;
+                prevP = P;
+                pending = true;
+                c->cur = cur;
+                c->has_frame = true;
+            }
+        }
+        return BMFR_OK;
+    }
     if (!c->side) {
         e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
         for (int i = 0; i < bmfr_ctx::kSeqEvents && e == hipSuccess; ++i) {

@@ -27,6 +27,7 @@
 #include <utility>
 
 #include "bmfr_launch.h"
+#include "bmfr_taa_tile.h"
 #include "bmfr_wave.h"
 
 namespace bmfr {
@@ -498,27 +499,18 @@ __device__ __forceinline__ void back_substitute(Lds<B>& L, int t) {
 #ifndef BMFR_COLS_WAVES
 #define BMFR_COLS_WAVES 4  // minimum waves per SIMD requested from the register allocator (128 VGPRs: 4 WGs/CU)
 #endif
+// One K1 work-group (block g of the launch), on the LDS area L.
 template <int NS, int FS, class IN, bool TONE>
-__global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params P, NoisyInputs in, Camera cam, int frame,
-                                                          const float* __restrict__ albedo,
-                                                          float* __restrict__ tone_out,
-                                                          const float* __restrict__ acc_prev,
-                                                          float* __restrict__ noisy_out,
-                                                          uint8_t* __restrict__ spp_out,
-                                                          float2* __restrict__ prev_pixel_out,
-                                                          float* __restrict__ acc_out,
-                                                          const double* __restrict__ noise,
-                                                          unsigned long long* __restrict__ stamps) {
+__device__ __forceinline__ void k1_cols_body(const Params& P, const NoisyInputs& in, const Camera& cam, int frame,
+                                             const float* __restrict__ albedo, float* __restrict__ tone_out,
+                                             const float* __restrict__ acc_prev, float* __restrict__ noisy_out,
+                                             uint8_t* __restrict__ spp_out, float2* __restrict__ prev_pixel_out,
+                                             float* __restrict__ acc_out, const double* __restrict__ noise,
+                                             unsigned long long* __restrict__ stamps, Lds<NS + FS + 3>& L, int g) {
     constexpr int B = NS + FS + 3;
-    __shared__ Lds<B> L;
     const int t = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int l = t & 63;
-#ifdef BMFR_NO_XCD_SWIZZLE
-    const int g = blockIdx.x;
-#else
-    const int g = xcd_swizzle(blockIdx.x, gridDim.x);
-#endif
 #ifdef BMFR_STAMPS
 #define BMFR_STAMP(k) \
     if (t == 0 && stamps) stamps[(size_t)g * 8 + (k)] = __builtin_amdgcn_s_memtime()
@@ -526,15 +518,6 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 #define BMFR_STAMP(k) (void)stamps
 #endif
     BMFR_STAMP(0);
-#if BMFR_STAGGER
-    // First round of work-groups: start the k-th group of 256 k * BMFR_STAGGER
-    // cycles late, so the four work-groups sharing a CU do not run their
-    // memory-bound phase 1 and VALU-bound fit in lockstep.
-    if (blockIdx.x < 4 * 256 && gridDim.x >= 8 * 256) {  // large launches only (not a tile's border ring)
-        const int n = ((int)(blockIdx.x >> 8) & 3) * (BMFR_STAGGER / 8000);
-        for (int s = 0; s < n; ++s) __builtin_amdgcn_s_sleep(125);
-    }
-#endif
     int bx, by;
     k1_block(P, g, bx, by);
     const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
@@ -753,6 +736,79 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 #undef BMFR_STAMP
 }
 
+// First round of work-groups: start the k-th group of 256 k * BMFR_STAGGER
+// cycles late, so the four work-groups sharing a CU do not run their
+// memory-bound phase 1 and VALU-bound fit in lockstep (large launches only,
+// not a tile's border ring).
+__device__ __forceinline__ void k1_stagger(int b, int n) {
+#if BMFR_STAGGER
+    if (b < 4 * 256 && n >= 8 * 256) {
+        const int k = ((b >> 8) & 3) * (BMFR_STAGGER / 8000);
+        for (int s = 0; s < k; ++s) __builtin_amdgcn_s_sleep(125);
+    }
+#endif
+}
+
+template <int NS, int FS, class IN, bool TONE>
+__global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params P, NoisyInputs in, Camera cam, int frame,
+                                                          const float* __restrict__ albedo,
+                                                          float* __restrict__ tone_out,
+                                                          const float* __restrict__ acc_prev,
+                                                          float* __restrict__ noisy_out,
+                                                          uint8_t* __restrict__ spp_out,
+                                                          float2* __restrict__ prev_pixel_out,
+                                                          float* __restrict__ acc_out,
+                                                          const double* __restrict__ noise,
+                                                          unsigned long long* __restrict__ stamps) {
+    __shared__ Lds<NS + FS + 3> L;
+    k1_stagger(blockIdx.x, gridDim.x);
+#ifdef BMFR_NO_XCD_SWIZZLE
+    const int g = blockIdx.x;
+#else
+    const int g = xcd_swizzle(blockIdx.x, gridDim.x);
+#endif
+    k1_cols_body<NS, FS, IN, TONE>(P, in, cam, frame, albedo, tone_out, acc_prev, noisy_out, spp_out, prev_pixel_out,
+                                   acc_out, noise, stamps, L, g);
+}
+
+// K1 of frame f and K2 (64 x kSeqTaaH tiles) of frame f - 1 in one launch:
+// work-groups [0, nk1) are K1 blocks, [nk1p, nk1p + nk2) TAA tiles (nk1p = nk1
+// rounded up to the 8 XCDs; the ones between exit).  The in-order dispatch
+// runs the tiles in K1's tail, where its last work-groups leave CUs idle, and
+// a frame costs one launch.  K2 of f - 1 reads frame f - 1's state, which K1
+// of f does not write (double-buffered), and frame f - 2's TAA output.
+constexpr int kSeqTaaH = 8;
+template <int NS, int FS, class IN>
+__global__ __launch_bounds__(kThreads, 4) void k_fused_cols_taa(Params P, NoisyInputs in, Camera cam, int frame,
+                                                                const float* __restrict__ acc_prev,
+                                                                float* __restrict__ noisy_out,
+                                                                uint8_t* __restrict__ spp_out,
+                                                                float2* __restrict__ prev_pixel_out,
+                                                                float* __restrict__ acc_out,
+                                                                const double* __restrict__ noise, Params P2,
+                                                                TaaArgs T, int nk1, int nk1p) {
+    constexpr int HW = 64 + 2, N = HW * (kSeqTaaH + 2);
+    __shared__ union {
+        Lds<NS + FS + 3> k1;
+        struct {
+            float4 Y[N];
+            double sE[kPowrENum];
+            double2 sRP[kPowrRPNum];
+        } k2;
+    } U;
+    const int b = blockIdx.x;
+    if (b < nk1) {
+        k1_stagger(b, nk1);
+        k1_cols_body<NS, FS, IN, false>(P, in, cam, frame, nullptr, nullptr, acc_prev, noisy_out, spp_out,
+                                        prev_pixel_out, acc_out, noise, nullptr, U.k1, xcd_swizzle(b, nk1));
+    } else if (b >= nk1p) {
+        const int gx = (P2.tx1 - P2.tx0 + 63) / 64, n2 = (int)gridDim.x - nk1p;
+        const int gi = xcd_swizzle(b - nk1p, n2);
+        taa_tile<true, IN, kSeqTaaH>(P2, T, P2.tx0 + (gi % gx) * 64, P2.ty0 + (gi / gx) * kSeqTaaH, U.k2.Y, U.k2.sE,
+                                     U.k2.sRP);
+    }
+}
+
 }  // namespace cols
 
 bool fused_cols_supported(const Params& P) {
@@ -770,6 +826,33 @@ static void launch_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
         hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, false>), dim3(k1_blocks(P)), dim3(cols::kThreads), 0, st,
                            P, A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
                            A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
+}
+
+bool seq_fused_supported(const Params& P) {
+    return fused_cols_supported(P) && P.fused_variant == 0 && P.ring == 0 && (P.scaled == 6 || P.scaled == 9);
+}
+
+template <int FS, class IN>
+static void launch_cols_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
+                            const FusedArgs* A2) {
+    const int nk1 = A ? k1_blocks(P) : 0, nk1p = (nk1 + 7) & ~7;
+    const int nk2 = A2 ? ((P2.tx1 - P2.tx0 + 63) / 64) * ((P2.ty1 - P2.ty0 + cols::kSeqTaaH - 1) / cols::kSeqTaaH) : 0;
+    if (nk1 + nk2 == 0) return;
+    const FusedArgs& a = A ? *A : *A2;
+    const TaaArgs T = A2 ? TaaArgs{A2->acc_out, A2->albedo, A2->prev_pixel_out, A2->result_out, A2->result_prev,
+                                   A2->frame}
+                         : TaaArgs{};
+    hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN>), dim3(nk2 ? nk1p + nk2 : nk1), dim3(cols::kThreads), 0,
+                       st, A ? P : P2, a.in, a.cam, a.frame, a.acc_prev, a.noisy_out, a.spp_out, a.prev_pixel_out,
+                       a.acc_out, a.noise_table, A2 ? P2 : P, T, nk1, nk1p);
+}
+
+hipError_t launch_fused_k1_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
+                               const FusedArgs* A2) {
+    const Params& Q = A ? P : P2;
+    if (Q.scaled == 6) Q.input_half ? launch_cols_taa<6, _Float16>(P, st, A, P2, A2) : launch_cols_taa<6, float>(P, st, A, P2, A2);
+    else Q.input_half ? launch_cols_taa<9, _Float16>(P, st, A, P2, A2) : launch_cols_taa<9, float>(P, st, A, P2, A2);
+    return hipGetLastError();
 }
 
 hipError_t launch_fused_k1_cols(const Params& P, hipStream_t st, const FusedArgs& A) {

@@ -12,6 +12,7 @@
 #include "bmfr_kernels.h"
 #include "bmfr_generic.h"
 #include "bmfr_launch.h"
+#include "bmfr_taa_tile.h"
 
 namespace bmfr {
 
@@ -106,22 +107,14 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
 }
 
 // --------------------------------------------------------- fused K2: TAA --
-// One 64x16 tile per 256-thread work-group.  The tile's tone-mapped colours
-// and a 1-pixel halo go to LDS once as YCoCg, and the 3x3 neighbourhoods
-// (bmfr.cl:897-920) are read from there; each thread keeps the RGB of its own
-// four output pixels in registers.  TONE: the tile is tone-mapped here from
-// the accumulated colour and the albedo (K1 then writes no tone-mapped
-// frame); otherwise K1's tone-mapped frame is read.  19 KB of LDS per
-// work-group, so up to eight fit a CU.
+// One 64 x kTaaH tile per 256-thread work-group (taa_tile, bmfr_taa_tile.h).
+// 64x16: 22 KB of LDS per work-group.
 #ifndef BMFR_K2_H  // tile height (multiple of 4)
 #define BMFR_K2_H 16
 #endif
 constexpr int kTaaW = 64, kTaaH = BMFR_K2_H;
 #ifndef BMFR_K2_WAVES  // minimum waves per SIMD the register allocation must allow
 #define BMFR_K2_WAVES 1
-#endif
-#ifndef BMFR_K2_EARLY_TAPS  // previous-frame taps loaded before the tone map
-#define BMFR_K2_EARLY_TAPS 1
 #endif
 template <bool TONE, class IN>
 __global__ __launch_bounds__(256, BMFR_K2_WAVES) void k_fused_taa(Params P, const float* __restrict__ src,
@@ -130,14 +123,9 @@ __global__ __launch_bounds__(256, BMFR_K2_WAVES) void k_fused_taa(Params P, cons
                                                                   float* __restrict__ result,
                                                                   const float* __restrict__ prev_frame,
                                                                   int frame) {
-    constexpr int HW = kTaaW + 2, HH = kTaaH + 2, N = HW * HH;
-    constexpr int RING = N - kTaaW * kTaaH;  // 164 halo pixels
-    constexpr int KN = kTaaH / 4;            // output pixels per thread
-    __shared__ float4 Y[N];                  // YCoCg (+ pad): one 16-byte read per neighbour
+    __shared__ float4 Y[(kTaaW + 2) * (kTaaH + 2)];  // YCoCg (+ pad): one 16-byte read per neighbour
     __shared__ double sE[TONE ? kPowrENum : 1];
     __shared__ double2 sRP[TONE ? kPowrRPNum : 1];
-    const int t = threadIdx.x;
-    if constexpr (TONE) bmfr_powr_tables_to_lds<256>(sE, sRP, t);
     // Output tile of this launch (the whole image, or a multi-GPU tile whose
     // one-pixel halo lies inside the buffer region).
 #ifdef BMFR_NO_XCD_SWIZZLE
@@ -146,68 +134,8 @@ __global__ __launch_bounds__(256, BMFR_K2_WAVES) void k_fused_taa(Params P, cons
     const int gi = xcd_swizzle(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int bxi = gi % gridDim.x, byi = gi / gridDim.x;
 #endif
-    const int x0 = P.tx0 + bxi * kTaaW, y0 = P.ty0 + byi * kTaaH;
-    const int tx = t & (kTaaW - 1), ty = t >> 6;
-    // Reprojected positions first, then the tile and its ring behind them.
-    float2 pf[KN];
-#pragma unroll
-    for (int k = 0; k < KN; ++k)
-        pf[k] = prev_pixel[pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + ty + 4 * k, P.ty1 - 1))];
-    f3 v[KN + 1], al[KN + 1];
-    int hx = 0, hy = 0;  // this thread's ring pixel (t < RING), in tile + halo coordinates
-    if (t < 2 * HW) {
-        hx = t % HW;
-        hy = t < HW ? 0 : HH - 1;
-    } else {
-        hx = t < 2 * HW + kTaaH ? 0 : HW - 1;
-        hy = 1 + (t - 2 * HW) % kTaaH;
-    }
-#pragma unroll
-    for (int k = 0; k <= KN; ++k) {
-        const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + 4 * k + 1 : hy;
-        if (k == KN && t >= RING) break;
-        const long lin = pix(P, min(max(x0 - 1 + lx, 0), P.width - 1), min(max(y0 - 1 + ly, 0), P.height - 1));
-        v[k] = ld3(src, lin);
-        if (TONE) al[k] = ld3in<IN>(albedo, lin);
-    }
-    f3 taps[KN][4];
-    if constexpr (BMFR_K2_EARLY_TAPS) {
-#pragma unroll
-        for (int k = 0; k < KN; ++k) taa_load_taps(P, pf[k], prev_frame, taps[k]);
-    }
-    if constexpr (TONE) __syncthreads();  // the powr tables are in LDS
-#pragma unroll
-    for (int k = 0; k <= KN; ++k) {
-        if (k == KN && t >= RING) break;
-        const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + 4 * k + 1 : hy;
-        v[k] = TONE ? tone_map(P, al[k], v[k], sE, sRP) : v[k];
-        const f3 yc = rgb_to_ycocg(v[k]);
-        Y[ly * HW + lx] = make_float4(yc.x, yc.y, yc.z, 0.f);
-    }
-    __syncthreads();
-    if constexpr (!BMFR_K2_EARLY_TAPS) {
-#pragma unroll
-        for (int k = 0; k < KN; ++k) taa_load_taps(P, pf[k], prev_frame, taps[k]);
-    }
-    // Tiles that reach the image border check every neighbour (bmfr.cl:901);
-    // the others have all nine in the image.
-    const bool edge = x0 == 0 || y0 == 0 || x0 + kTaaW >= P.width || y0 + kTaaH >= P.height;
-#pragma unroll
-    for (int k = 0; k < KN; ++k) {
-        const int x = x0 + tx, y = y0 + ty + 4 * k;
-        if (x < P.tx1 && y < P.ty1) {
-            const int c = (ty + 4 * k + 1) * HW + tx + 1;
-            f3 nb[9];
-#pragma unroll
-            for (int j = 0; j < 9; ++j) {
-                const float4 q = Y[c + (j / 3 - 1) * HW + (j % 3 - 1)];
-                nb[j] = f3{q.x, q.y, q.z};
-            }
-            const f3 r = edge ? taa_resolve<true>(P, x, y, v[k], pf[k], nb, taps[k], frame)
-                              : taa_resolve<false>(P, x, y, v[k], pf[k], nb, taps[k], frame);
-            st3(result, pix(P, x, y), r);
-        }
-    }
+    const TaaArgs T{src, albedo, prev_pixel, result, prev_frame, frame};
+    taa_tile<TONE, IN, kTaaH>(P, T, P.tx0 + bxi * kTaaW, P.ty0 + byi * kTaaH, Y, sE, sRP);
 }
 
 // ------------------------------------------------ stencil K2 (tonecols) --

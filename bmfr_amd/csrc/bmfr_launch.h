@@ -81,6 +81,11 @@ hipError_t launch_noise_table(const Params& P, hipStream_t st, const FusedArgs& 
 constexpr int kNoiseFrames = 64;
 hipError_t launch_noise_tables(const Params& P, hipStream_t st, int first, int frames, double* table);
 hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedArgs& A);
+// Sequence kernel (bmfr_process_sequence): K1 of a frame (A, or none) and K2
+// of the frame before it (A2, or none) in one launch.
+bool seq_fused_supported(const Params& P);
+hipError_t launch_fused_k1_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
+                               const FusedArgs* A2);
 hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A);
 hipError_t launch_taa(const Params& P, hipStream_t st, const float2* prev_pixel, const float* new_frame,
                       float* result, const float* prev_frame, int frame);
