@@ -219,9 +219,12 @@ bmfr_status bmfr_process_frame_border(bmfr_ctx *ctx, void *stream, const bmfr_fr
  * as tasks() holds the sequence in memory): in[i], the column-major
  * prev_frame_camera_matrices[16*i..] and pixel_offsets[2*i..] are frame
  * first_frame+i's arguments of bmfr_process_frame.  The frames are
- * pipelined: TAA of frame f (K2) runs on a context-owned stream beside K1 of
- * frame f+1; all work is joined back onto `stream`, so everything the call
- * enqueues is complete when `stream` reaches the point after it.  All
+ * pipelined: one launch per frame on `stream` runs K1 of frame f and, in its
+ * tail, TAA of frame f-1 (half tmp_data, canonical feature lists), else TAA
+ * of frame f (K2) runs on a context-owned stream beside K1 of frame f+1
+ * (also with the environment variable BMFR_SEQUENCE=streams); all work is
+ * joined back onto `stream`, so everything the call enqueues is complete
+ * when `stream` reaches the point after it.  All
  * inputs must stay valid until then.  outputs (nullable; entries nullable):
  * outputs[i] receives frame i's output (W*H float3, device or page-locked
  * host memory).  Results equal bmfr_process_frame per frame bit for bit.

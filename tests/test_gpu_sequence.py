@@ -1,7 +1,10 @@
-"""bmfr_process_sequence (include/bmfr.h): frames pipelined over two streams
-(K2 of frame f beside K1 of frame f+1) must give every frame's output and
-the final temporal state bit for bit as bmfr_process_frame does, frame by
-frame -- across chunk boundaries and mixed with per-frame calls."""
+"""bmfr_process_sequence (include/bmfr.h): frames pipelined -- by default one
+launch per frame with K1 of frame f and the TAA tiles of frame f-1
+(k_fused_cols_taa), or (BMFR_SEQUENCE=streams, and configurations the
+combined kernel does not cover) over two streams, K2 of frame f beside K1 of
+frame f+1 -- must give every frame's output and the final temporal state bit
+for bit as bmfr_process_frame does, frame by frame -- across chunk
+boundaries and mixed with per-frame calls."""
 from __future__ import annotations
 
 import numpy as np
@@ -31,13 +34,19 @@ def _frames(W, H, half):
     return out
 
 
+@pytest.mark.parametrize("streams", [False, True])
 @pytest.mark.parametrize("W,H,kw", [
     (160, 96, {}),
+    (136, 76, {}),  # partial TAA tiles at the right and bottom edges
     (128, 80, {"use_half_precision_in_tmp_data": 0}),
     (160, 96, {"scaled": bmfr_amd.SCALED_THIRD_ORDER, "input_half": 1}),
     (96, 64, {"scaled": bmfr_amd.SCALED_THIRD_ORDER[:3] + bmfr_amd.SCALED_THIRD_ORDER[6:]}),  # generic K1: serial
 ])
-def test_sequence_matches_per_frame(W, H, kw, gpu):
+def test_sequence_matches_per_frame(W, H, kw, streams, gpu, monkeypatch):
+    if streams:
+        monkeypatch.setenv("BMFR_SEQUENCE", "streams")
+    else:
+        monkeypatch.delenv("BMFR_SEQUENCE", raising=False)
     cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, **kw)
     seq = _frames(W, H, kw.get("input_half", 0))
     n = W * H * 3
