@@ -23,6 +23,37 @@ struct TaaArgs {
 #ifndef BMFR_K2_EARLY_TAPS  // previous-frame taps loaded before the tone map
 #define BMFR_K2_EARLY_TAPS 1
 #endif
+#ifndef BMFR_K2_SHARE_TAPS  // right-hand taps taken from the next lane's left-hand taps when they coincide
+#define BMFR_K2_SHARE_TAPS 0  // measured slower: K2 0.131 vs 0.109 ms (the lane moves and the serialised fallback)
+#endif
+
+// taa_load_taps for a wave whose lane l + 1 holds the pixel right of lane
+// l's: the previous-frame taps (ix + 1, iy) and (ix + 1, iy + 1) of lane l
+// are lane l + 1's (ix, iy) and (ix, iy + 1) whenever the clamped addresses
+// coincide (the same whole-pixel motion), and are then moved across lanes
+// instead of loaded again; the other lanes (always lane 63) load them.  The
+// values are the same loads' values: bit-identical to taa_load_taps.
+__device__ __forceinline__ void taa_load_taps_shared(const Params& P, float2 pf, const float* __restrict__ prev_frame,
+                                                     f3 (&pc)[4]) {
+    const int ix = (int)fminf(fmaxf(floorf(pf.x), -2.f), (float)P.width + 1.f);
+    const int iy = (int)fminf(fmaxf(floorf(pf.y), -2.f), (float)P.height + 1.f);
+    const int xa = clamp_rx(P, ix), xb = clamp_rx(P, ix + 1), ya = clamp_ry(P, iy), yb = clamp_ry(P, iy + 1);
+    const int lane = __lane_id();
+    const int nxa = __shfl_down(xa, 1, 64), nya = __shfl_down(ya, 1, 64), nyb = __shfl_down(yb, 1, 64);
+    const bool own = lane == 63 || nxa != xb || nya != ya || nyb != yb;  // this lane loads its right-hand taps
+    pc[0] = ld3(prev_frame, pix(P, xa, ya));
+    pc[2] = ld3(prev_frame, pix(P, xa, yb));
+    if (own) {
+        pc[1] = ld3(prev_frame, pix(P, xb, ya));
+        pc[3] = ld3(prev_frame, pix(P, xb, yb));
+    }
+    const f3 r0{__shfl_down(pc[0].x, 1, 64), __shfl_down(pc[0].y, 1, 64), __shfl_down(pc[0].z, 1, 64)};
+    const f3 r2{__shfl_down(pc[2].x, 1, 64), __shfl_down(pc[2].y, 1, 64), __shfl_down(pc[2].z, 1, 64)};
+    if (!own) {
+        pc[1] = r0;
+        pc[3] = r2;
+    }
+}
 
 // Y: (64 + 2) * (TH + 2) float4; sE / sRP: the powr tables' LDS copies (TONE).
 template <bool TONE, class IN, int TH>
@@ -61,7 +92,10 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
     f3 taps[KN][4];
     if constexpr (BMFR_K2_EARLY_TAPS) {
 #pragma unroll
-        for (int k = 0; k < KN; ++k) taa_load_taps(P, pf[k], T.prev_frame, taps[k]);
+        for (int k = 0; k < KN; ++k) {
+            if constexpr (BMFR_K2_SHARE_TAPS) taa_load_taps_shared(P, pf[k], T.prev_frame, taps[k]);
+            else taa_load_taps(P, pf[k], T.prev_frame, taps[k]);
+        }
     }
     if constexpr (TONE) __syncthreads();  // the powr tables are in LDS
 #pragma unroll
@@ -75,7 +109,10 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
     __syncthreads();
     if constexpr (!BMFR_K2_EARLY_TAPS) {
 #pragma unroll
-        for (int k = 0; k < KN; ++k) taa_load_taps(P, pf[k], T.prev_frame, taps[k]);
+        for (int k = 0; k < KN; ++k) {
+            if constexpr (BMFR_K2_SHARE_TAPS) taa_load_taps_shared(P, pf[k], T.prev_frame, taps[k]);
+            else taa_load_taps(P, pf[k], T.prev_frame, taps[k]);
+        }
     }
     // Tiles that reach the image border check every neighbour (bmfr.cl:901);
     // the others have all nine in the image.
