@@ -11,13 +11,20 @@ Workload at N=1: 3840x2160, reference default parameters (B = 13 features,
 half tmp_data, 32x32 blocks), frames W..W+K-1 of the sequence (temporal path
 active on every timed frame).
 
-Multi-GPU (torchrun, one process per GPU): the frame is cut into a tile grid
-(1x1, 2x1, 2x2, 4x2), one tile per rank, and each rank denoises its tile
-with a tiled context; before every frame the ranks exchange the halo ring
-of the previous frame's temporal state over RCCL (bmfr_amd/tiling.py,
-DESIGN.md "Multi-GPU").  Default --scaling weak: every rank's tile is
---width x --height (3840x2160), so 4 GPUs run a 7680x4320 frame; --scaling
-strong splits one --width x --height frame.  Timing: barrier + synchronize
+The N = 1 line also carries the metric's other sizes, untiled on the same
+GPU: `ms_per_frame_1080p` (1920x1080) and `ms_per_frame_8k` (7680x4320, the
+1-GPU point of the north star's scaling target).
+
+Multi-GPU (torchrun, one process per GPU): BASELINE config 4 -- one
+7680x4320 frame cut into a tile grid (2x1, 2x2, 4x2 for N = 2, 4, 8), one
+tile per rank (--scaling strong, the default for N > 1), each rank
+denoising its tile with a tiled context; before every frame the ranks
+exchange the halo ring of the previous frame's temporal state over RCCL
+(bmfr_amd/tiling.py, DESIGN.md "Multi-GPU"), overlapped with the tile's
+interior blocks.  Rank 0 first times the same frames untiled on its own GPU
+(`ms_per_frame_1gpu`, `speedup_vs_1gpu`); per-rank exchange / interior /
+border times and halo bytes come back in `ranks`.  --scaling weak instead
+gives every rank a --width x --height tile.  Timing: barrier + synchronize
 around K frames (exchange included), max over ranks.
 
 `kernel_ms`, `device_ms_per_frame` and the roofline's K1 time come from HIP
@@ -69,8 +76,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--width", type=int, default=3840)
-    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--width", type=int, default=None, help="default 3840 (N = 1), 7680 (N > 1)")
+    ap.add_argument("--height", type=int, default=None, help="default 2160 (N = 1), 4320 (N > 1)")
     ap.add_argument("--half-tmp", type=int, default=1)
     ap.add_argument("--third-order", action="store_true", help="B = 16 feature set (BASELINE config 5)")
     ap.add_argument("--input-half", action="store_true",
@@ -79,10 +86,14 @@ def parse():
                     help="tone map with the device library's powr (bit-identical to the reference kernel "
                          "on gfx950) instead of the correctly rounded one")
     ap.add_argument("--no-1080p", action="store_true", help="skip the 1920x1080 line (N = 1 only)")
+    ap.add_argument("--no-8k", action="store_true", help="skip the untiled 7680x4320 line (N = 1) / the 1-GPU "
+                                                         "reference time (N > 1)")
+    ap.add_argument("--frames-8k", type=int, default=30, help="timed frames of the untiled 8K line (N = 1)")
     ap.add_argument("--cpu-frames", type=int, default=2, help="timed CPU-oracle frames (0 = skip)")
     ap.add_argument("--seed", type=int, default=0x424D4652)
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="multi-GPU: weak = one --width x --height tile per GPU, strong = one frame split")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                    help="multi-GPU: strong = one --width x --height frame split (default), "
+                         "weak = one --width x --height tile per GPU")
     ap.add_argument("--halo", type=int, default=64, help="tile halo in pixels (>= 34 + max motion)")
     ap.add_argument("--sequence", action="store_true",
                     help="single GPU: the timed frames as one bmfr_process_sequence call (TAA of frame f beside "
@@ -173,9 +184,12 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     compute = torch.cuda.current_stream(dev)
     comm = torch.cuda.Stream(dev) if grid else None
     frame_done = torch.cuda.Event() if grid else None
+    # Split timings of sampled timed frames: (interior start/end, exchange
+    # start/end, border end) events, on the streams the work runs on.
+    marks = []
     torch.cuda.synchronize()
 
-    def run(f):
+    def run(f, mark=False):
         fr = frames[f]
         prev = frames[f - 1] if f > 0 else None
         args = (fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], cams[f][0], cams[f][1], f)
@@ -186,36 +200,48 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
             transport.exchange_ctx(den)
             den.process_frame(*args, **kw)
         else:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if mark else None
             comm.wait_event(frame_done)  # the previous frame's state is complete
+            if ev:
+                ev[0].record(compute)
             den.process_frame_interior(*args, **kw)
+            if ev:
+                ev[1].record(compute)
             with torch.cuda.stream(comm):  # one pack and one unpack kernel around the RCCL batch
+                if ev:
+                    ev[2].record(comm)
                 transport.exchange_ctx(den)
+                if ev:
+                    ev[3].record(comm)
             compute.wait_stream(comm)
             den.process_frame_border(*args, **kw)
+            if ev:
+                ev[4].record(compute)
+                marks.append(ev)
         if frame_done is not None:
             frame_done.record(compute)
 
     # Untiled: the whole run as bmfr_process_sequence calls (frames pipelined),
     # unless per_frame; tiled: frame by frame around the halo exchange.
     pipelined = grid is None and not per_frame
+    stride = PROF_STRIDE if steps >= PROF_STRIDE else 1
 
-    def run_range(f0, f1):
+    def run_range(f0, f1, timed=False):
         if pipelined:
             den.process_sequence(frames[f0:f1], cams[f0:f1], f0)
         else:
             for f in range(f0, f1):
-                run(f)
+                run(f, mark=timed and f % stride == 0)
 
     if warmup:
         run_range(0, warmup)
-    stride = PROF_STRIDE if steps >= PROF_STRIDE else 1
     den.set_profiling(True, capacity=steps, stride=stride)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_range(warmup, warmup + steps)
+    run_range(warmup, warmup + steps, timed=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -226,6 +252,7 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         elapsed = float(t.item())
     kprof = den.profile()
     den.set_profiling(False)
+    overshoot = den.halo_status() if grid else 0  # raises if a frame reprojected past the halo
 
     # Quality: PSNR of this rank's tile of the last output against the clean render.
     clean = bmfr_amd.synth_region_device(W, H, region, nfr - 1, seed=seed, device=local, clean=True)["clean"]
@@ -238,7 +265,14 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
 
     last = frames[nfr - 1]
     noisy_tm = torch.clamp(torch.clamp(last["albedo"].float() * last["noisy"].float(), min=0) ** 0.454545, 0, 1)
-    return {
+    split = None
+    if marks:
+        mean = lambda i, j: float(np.mean([e[i].elapsed_time(e[j]) for e in marks]))  # noqa: E731
+        split = {"interior_ms": mean(0, 1), "exchange_ms": mean(2, 3), "border_ms": mean(1, 4),
+                 "frame_ms": mean(0, 4),
+                 "halo_bytes_sent": int(sum(transport._layout[1])), "halo_bytes_received": int(sum(transport._layout[3])),
+                 "halo_overshoot_px": overshoot}
+    res = {
         "cfg": cfg,
         "ms_per_frame": 1e3 * elapsed / steps,
         "k1_ms": float(np.mean([p[1] for p in kprof])),
@@ -246,27 +280,41 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         "dev_ms": float(np.mean([p[3] for p in kprof])),
         "psnr": psnr(tile_of(out).cpu().numpy(), tile_of(clean).cpu().numpy()),
         "psnr_in": psnr(tile_of(noisy_tm).cpu().numpy(), tile_of(clean).cpu().numpy()),
+        "split": split,
     }
+    del frames, den, out, clean, noisy_tm, last
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
 
 
-def valu_issue():
-    """VALU view of both kernels from the committed rocprofv3 SQ pass
-    (profiles/r01_sq_counters.json): instructions per SIMD x the achievable
-    issue cost of a wave64 f32 instruction (3.24 cycles, profiles/r01_valu_rate.txt)
-    / the kernel's cycles -- the fraction of the VALU roof each kernel uses."""
-    p = os.path.join(ROOT, "profiles", "r01_sq_counters.json")
-    if not os.path.exists(p):
-        return None
-    with open(p) as f:
+def valu_roofline():
+    """K1's other roof: VALU issue.  From the committed rocprofv3 SQ pass of
+    the same bench command (profiles/*sq_counters.json, newest round):
+    K1's VALU instructions per SIMD x the achievable issue cost of a wave64
+    f32 instruction (3.24 cycles, profiles/r01_valu_rate.txt) / K1's cycles.
+    K1 runs below both roofs -- its limiter is the latency of phase 1's
+    dependent gathers and the fit's per-column barriers."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_sq_counters.json")))
+    if not files:
+        return {}
+    with open(files[-1]) as f:
         d = json.load(f)
-    out = {}
-    for name, k in (("fused_block_k1", "K1 k_fused_cols"), ("taa_k2", "K2 k_fused_taa")):
-        if k in d:
-            c = d[k]
-            out[name] = round(c["valu_instr_per_simd"] * 3.24 / c["kernel_cycles_per_xcd"], 3)
-    out["source"] = "rocprofv3 SQ_INSTS_VALU / GRBM_GUI_ACTIVE (profiles/r01_sq_counters.json), " \
-                    "3.24 cycles per wave64 VALU instruction (tools/valu_rate.hip)"
-    return out
+    c = d.get("K1 k_fused_cols")
+    if not c:
+        return {}
+    return {"valu_frac": round(c["valu_instr_per_simd"] * 3.24 / c["kernel_cycles_per_xcd"], 3),
+            "limiter": "latency (phase-1 gathers, per-column barriers) under the HBM and VALU roofs",
+            "valu_source": os.path.relpath(files[-1], ROOT) + ": SQ_INSTS_VALU / GRBM_GUI_ACTIVE, "
+                                                                "3.24 cycles per wave64 VALU instruction"}
+
+
+def side_line(r):
+    """A secondary-size field of the N = 1 line."""
+    return {"value": round(r["ms_per_frame"], 4), "device_ms_per_frame": round(r["dev_ms"], 4),
+            "kernel_ms": {"fused_block_k1": round(r["k1_ms"], 4), "taa_k2": round(r["k2_ms"], 4)},
+            "psnr_db": round(r["psnr"], 2)}
 
 
 def main():
@@ -284,6 +332,9 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    # N = 1: the 4K headline (BASELINE config 3); N > 1: config 4's 8K frame.
+    a.width = a.width or (3840 if world == 1 else 7680)
+    a.height = a.height or (2160 if world == 1 else 4320)
 
     tx, ty = tiling.grid_for(world)
     if a.scaling == "weak":
@@ -292,13 +343,34 @@ def main():
         W, H = a.width, a.height
     grid = tiling.TileGrid(W, H, tx, ty, halo=a.halo) if world > 1 else None
     tile = grid.tile(rank) if grid else (0, 0, W, H)
+    # N > 1: rank 0 first times the same frames of the whole frame on its own
+    # GPU (the 1-GPU point of the scaling curve); the other ranks wait.
+    r1 = None
+    if world > 1 and rank == 0 and not a.no_8k:
+        r1 = run_sequence(a, W, H, (0, 0, W, H), None, 0, 1, dev, backend, a.steps, a.warmup, per_frame=True)
+    if world > 1:
+        dist.barrier()
     r = run_sequence(a, W, H, tile, grid, rank, world, dev, backend, a.steps, a.warmup, per_frame=not a.sequence)
     cfg = r["cfg"]
-    # The metric's second resolution (BASELINE.json: ms/frame @1080p & 4K), single GPU only.
-    r1080 = None
+    # The metric's other resolutions (BASELINE.json: ms/frame @1080p & 4K, and
+    # the 8K frame of the scaling target), single GPU only.
+    r1080 = r8k = None
     if world == 1 and not a.no_1080p and (W, H) != (1920, 1080):
         r1080 = run_sequence(a, 1920, 1080, (0, 0, 1920, 1080), None, 0, 1, dev, backend, a.steps, a.warmup,
                              per_frame=not a.sequence)
+    if world == 1 and not a.no_8k and (W, H) != (7680, 4320):
+        n8 = min(a.steps, a.frames_8k)
+        r8k = run_sequence(a, 7680, 4320, (0, 0, 7680, 4320), None, 0, 1, dev, backend, n8, a.warmup,
+                           per_frame=not a.sequence)
+        r8k["steps"] = n8
+    ranks = None
+    if world > 1 and r["split"] is not None:
+        keys = ("interior_ms", "exchange_ms", "border_ms", "frame_ms", "halo_bytes_sent", "halo_overshoot_px")
+        v = torch.zeros(world, len(keys), dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        v[rank] = torch.tensor([float(r["split"][k]) for k in keys], dtype=torch.float64)
+        dist.all_reduce(v)
+        ranks = [{k: (round(float(x), 4) if k.endswith("_ms") else int(x)) for k, x in zip(keys, row)}
+                 for row in v.cpu().tolist()]
 
     s = 2 if a.input_half else 4
     tile_px = tile[2] * tile[3]
@@ -316,7 +388,7 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_frame, 4),
             "higher_is_better": False,
-            "scaling": a.scaling,
+            "scaling": a.scaling if world > 1 else "strong",
             "vs_baseline": None,
             "dtype": "f32" + ("+f16 tmp_data" if a.half_tmp else "") + ("+f16 input planes" if a.input_half else ""),
             "data": "synthetic (GPU-rendered 1-spp frames + features, resident in HBM)",
@@ -339,13 +411,17 @@ def main():
                          "frame_frac": round(frame_bytes_per_px(s) * W * H / (ms_per_frame * 1e-3) / 1e9
                                              / (HBM_PEAK_GBS * world), 4)},
         }
-        if r1080 is not None:
-            line["ms_per_frame_1080p"] = {
-                "value": round(r1080["ms_per_frame"], 4), "device_ms_per_frame": round(r1080["dev_ms"], 4),
-                "kernel_ms": {"fused_block_k1": round(r1080["k1_ms"], 4), "taa_k2": round(r1080["k2_ms"], 4)},
-                "psnr_db": round(r1080["psnr"], 2)}
         if world == 1:
-            line["valu_issue_frac"] = valu_issue()
+            line["roofline"].update(valu_roofline())
+        if r1080 is not None:
+            line["ms_per_frame_1080p"] = side_line(r1080)
+        if r8k is not None:
+            line["ms_per_frame_8k"] = dict(side_line(r8k), frames_timed=r8k["steps"])
+        if r1 is not None:
+            line["ms_per_frame_1gpu"] = side_line(r1)
+            line["speedup_vs_1gpu"] = round(r1["ms_per_frame"] / ms_per_frame, 3)
+        if ranks is not None:
+            line["ranks"] = ranks
         if world == 1 and a.cpu_frames > 0:
             line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_frames, a.seed)
         print(json.dumps(line), flush=True)

@@ -27,7 +27,9 @@ POSITION_X2, POSITION_Y2, POSITION_Z2 = 7, 8, 9
 POSITION_X3, POSITION_Y3, POSITION_Z3 = 10, 11, 12
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "unsupported configuration",
-          3: "out of device memory", 4: "HIP runtime error", 5: "no HIP device"}
+          3: "out of device memory", 4: "HIP runtime error", 5: "no HIP device",
+          6: "reprojection reached past the tile halo"}
+HALO_EXCEEDED = 6
 
 
 class BmfrError(RuntimeError):
@@ -104,6 +106,7 @@ SIGNATURES = {
     "bmfr_process_sequence": (_I, [_P, _P, _I, C.POINTER(FrameInputs), _F16, _F2, _I, C.POINTER(_P)]),
     "bmfr_process_frame_border": (_I, [_P, _P, C.POINTER(FrameInputs), _F16, _F2, _I]),
     "bmfr_output": (_P, [_P]),
+    "bmfr_halo_status": (_I, [_P, C.POINTER(C.c_uint)]),
     "bmfr_state": (_I, [_P, _I, C.POINTER(StateView)]),
     "bmfr_set_profiling": (_I, [_P, _I, _I]),
     "bmfr_set_profiling_stride": (_I, [_P, _I]),

@@ -26,7 +26,7 @@ struct bmfr_ctx {
     uint8_t* spp[2] = {nullptr, nullptr};
     float* acc[2] = {nullptr, nullptr};
     float* result[2] = {nullptr, nullptr};
-    float* tone[2] = {nullptr, nullptr};  // K1-tone-mapped variants only
+    float* tone[2] = {nullptr, nullptr};  // generic feature lists only (the canonical path tone-maps in K2)
     float2* prev_pixel[2] = {nullptr, nullptr};  // double-buffered: K2 of frame f reads it while K1 of f+1 writes
     // bmfr_process_sequence: side stream for K2 and a ring of ordering events
     hipStream_t side = nullptr;
@@ -39,6 +39,13 @@ struct bmfr_ctx {
     bool has_frame = false;
     // bmfr_process_frame_interior issued for this frame, border part pending
     int pending_frame = -1;
+    int pending_prof_slot = -1;  // profiling slot part 0 took for that frame (-1: none)
+    // Tiled contexts: reprojection reach past the valid state.  K1 raises
+    // reach_dev (device word); K2 moves it into reach_host[0] (page-locked,
+    // max over frames since frame 0) and stamps reach_host[1] = frame + 1.
+    unsigned* reach_dev = nullptr;
+    volatile unsigned* reach_host = nullptr;
+    hipEvent_t reach_event = nullptr;  // after the last frame's K2
     // Profiling ring: 3 events per frame (before K1, after K1, after K2).
     int prof_capacity = 0;
     int prof_stride = 1;  // record frames whose number is a multiple of this
@@ -50,6 +57,18 @@ struct bmfr_ctx {
 namespace {
 
 thread_local int g_last_hip_error = 0;
+
+// Makes the context's device current for the duration of an entry point
+// (a process may hold contexts on several GPUs), restoring the caller's.
+struct DeviceGuard {
+    int prev = -1, dev;
+    explicit DeviceGuard(int d) : dev(d) {
+        if (hipGetDevice(&prev) != hipSuccess || prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+};
 
 bmfr_status hip_status(hipError_t e) {
     if (e == hipSuccess) return BMFR_OK;
@@ -126,17 +145,6 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     P.half_tmp = c->use_half_precision_in_tmp_data ? 1 : 0;
     P.input_half = c->input_half ? 1 : 0;
     P.library_powr = c->library_powr ? 1 : 0;
-    // Diagnostic A/B overrides of the fused path: BMFR_FUSED_KERNEL=block
-    // (generic-feature K1), k1tone (row-split K1 with tone mapping in K1) or
-    // rows (row-split K1, bmfr_fused.hip, instead of the column-split one).
-    const char* v = std::getenv("BMFR_FUSED_KERNEL");
-    P.fused_variant = !v                                ? 0
-                      : std::strcmp(v, "block") == 0   ? 1
-                      : std::strcmp(v, "k1tone") == 0  ? 2
-                      : std::strcmp(v, "rows") == 0    ? 3
-                      : std::strcmp(v, "tonecols") == 0 ? 4
-                      : std::strcmp(v, "colstone") == 0 ? 5
-                                                       : 0;
     P.ox = s->region_x;
     P.oy = s->region_y;
     P.stride = s->region_width;
@@ -148,6 +156,12 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     P.tx0 = P.ty0 = 0;
     P.tx1 = P.width;
     P.ty1 = P.height;
+    // valid previous state: the whole region (checked only for tiles)
+    P.check_reach = c->tile_width > 0 ? 1 : 0;
+    P.vx0 = P.ox;
+    P.vy0 = P.oy;
+    P.vx1 = P.ox + P.stride;
+    P.vy1 = P.oy + P.rows;
     return P;
 }
 
@@ -259,6 +273,7 @@ const char* bmfr_status_string(bmfr_status s) {
         case BMFR_ERROR_OUT_OF_MEMORY: return "out of device memory";
         case BMFR_ERROR_HIP: return "HIP runtime error";
         case BMFR_ERROR_NO_DEVICE: return "no HIP device";
+        case BMFR_ERROR_HALO_EXCEEDED: return "reprojection reached past the tile halo";
     }
     return "unknown status";
 }
@@ -290,13 +305,25 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
         if (e == hipSuccess) e = hipMalloc(&c->acc[i], px * 3 * sizeof(float));
         if (e == hipSuccess) e = hipMalloc(&c->result[i], px * 3 * sizeof(float));
     }
-    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipMalloc(&c->tone[i], px * 3 * sizeof(float));
+    if (!bmfr::fused_supported(c->P))  // the generic path's K1 writes a tone-mapped frame for its TAA
+        for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipMalloc(&c->tone[i], px * 3 * sizeof(float));
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipMalloc(&c->prev_pixel[i], px * sizeof(float2));
     if (e == hipSuccess && std::getenv("BMFR_STAMPS"))
         e = hipMalloc(&c->stamps, (size_t)sz.blocks * 8 * sizeof(unsigned long long));
     if (e == hipSuccess)
         e = hipMalloc(&c->noise_table,
                       (size_t)bmfr::kNoiseFrames * bmfr::kMaxFeatures * bmfr::kBlockPixels * sizeof(double));
+    if (e == hipSuccess && is_tiled(cfg)) {
+        void* h = nullptr;
+        e = hipMalloc(&c->reach_dev, sizeof(unsigned));
+        if (e == hipSuccess) e = hipMemset(c->reach_dev, 0, sizeof(unsigned));
+        if (e == hipSuccess) e = hipHostMalloc(&h, 2 * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) {
+            c->reach_host = static_cast<volatile unsigned*>(h);
+            c->reach_host[0] = c->reach_host[1] = 0;
+            e = hipEventCreateWithFlags(&c->reach_event, hipEventDisableTiming);
+        }
+    }
     if (e != hipSuccess) {
         bmfr_destroy(c);
         return hip_status(e);
@@ -307,6 +334,10 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
 
 bmfr_status bmfr_destroy(bmfr_ctx* c) {
     if (!c) return BMFR_ERROR_INVALID_ARGUMENT;
+    DeviceGuard guard(c->device);
+    (void)hipFree(c->reach_dev);
+    if (c->reach_host) (void)hipHostFree(const_cast<unsigned*>(c->reach_host));
+    if (c->reach_event) (void)hipEventDestroy(c->reach_event);
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(c->noisy_acc[i]);
         (void)hipFree(c->spp[i]);
@@ -357,6 +388,7 @@ bmfr_status bmfr_accumulate_noisy_data(bmfr_ctx* c, void* stream, float* out_pre
         return BMFR_ERROR_INVALID_ARGUMENT;
     bmfr::NoisyInputs in{current_normals, previous_normals, current_positions, previous_positions,
                          current_noisy, previous_noisy, previous_spp};
+    DeviceGuard guard(c->device);
     return hip_status(bmfr::launch_accumulate_noisy(
         c->P, as_stream(stream), reinterpret_cast<float2*>(out_prev_frame_pixel), accept_bools, in,
         current_noisy, current_spp, tmp_data, make_camera(prev_frame_camera_matrix, pixel_offset),
@@ -369,6 +401,7 @@ bmfr_status bmfr_fitter(bmfr_ctx* c, void* stream, float* weights, float* mins_m
         return BMFR_ERROR_INVALID_ARGUMENT;
     if (!stage_api_ok(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
     if (!bmfr::fitter_supported(c->P.not_scaled, c->P.scaled)) return BMFR_ERROR_UNSUPPORTED;
+    DeviceGuard guard(c->device);
     return hip_status(bmfr::launch_fitter(c->P, as_stream(stream), weights, mins_maxs, tmp_data, frame_number));
 }
 
@@ -381,6 +414,7 @@ bmfr_status bmfr_weighted_sum(bmfr_ctx* c, void* stream, const float* weights, c
         frame_number < 0)
         return BMFR_ERROR_INVALID_ARGUMENT;
     if (!stage_api_ok(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
+    DeviceGuard guard(c->device);
     return hip_status(bmfr::launch_weighted_sum(c->P, as_stream(stream), weights, mins_maxs, output,
                                                 current_normals, current_positions, frame_number));
 }
@@ -395,6 +429,7 @@ bmfr_status bmfr_accumulate_filtered_data(bmfr_ctx* c, void* stream, const float
         return BMFR_ERROR_INVALID_ARGUMENT;
     if (!stage_api_ok(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
     if (frame_number > 0 && !accumulated_prev_frame) return BMFR_ERROR_INVALID_ARGUMENT;
+    DeviceGuard guard(c->device);
     return hip_status(bmfr::launch_accumulate_filtered(
         c->P, as_stream(stream), filtered_frame, reinterpret_cast<const float2*>(in_prev_frame_pixel),
         accept_bools, albedo, tone_mapped_frame, current_spp, accumulated_prev_frame, accumulated_frame,
@@ -407,6 +442,7 @@ bmfr_status bmfr_taa(bmfr_ctx* c, void* stream, const float* in_prev_frame_pixel
         return BMFR_ERROR_INVALID_ARGUMENT;
     if (!stage_api_ok(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
     if (frame_number > 0 && !prev_frame) return BMFR_ERROR_INVALID_ARGUMENT;
+    DeviceGuard guard(c->device);
     return hip_status(bmfr::launch_taa(c->P, as_stream(stream),
                                        reinterpret_cast<const float2*>(in_prev_frame_pixel), new_frame,
                                        result_frame, prev_frame, frame_number));
@@ -448,8 +484,23 @@ bmfr::FusedArgs frame_args(const bmfr_ctx* c, const bmfr_frame_inputs* in, const
     A.tone_out = c->tone[cur];
     A.result_out = c->result[cur];
     A.noise_table = c->noise_table;
+    A.reach = c->reach_dev;
+    A.reach_host = const_cast<unsigned*>(c->reach_host);
     A.stamps = c->stamps;
     return A;
+}
+
+// Tiled contexts: BMFR_ERROR_HALO_EXCEEDED once a completed frame reported
+// reprojection taps past the exchanged state (sticky until frame 0).
+bmfr_status reach_check(bmfr_ctx* c, int frame_number) {
+    if (!c->reach_host) return BMFR_OK;
+    if (frame_number == 0 && c->reach_host[0] > 0) {  // a new sequence: clear the report
+        const bmfr_status st = hip_status(hipEventSynchronize(c->reach_event));
+        if (st != BMFR_OK) return st;
+        c->reach_host[0] = 0;
+        return BMFR_OK;
+    }
+    return c->reach_host[0] > 0 ? BMFR_ERROR_HALO_EXCEEDED : BMFR_OK;
 }
 
 // Blocks of frame `frame`'s K1 launch (frame_params) whose reads of the
@@ -522,20 +573,25 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
     if (st != BMFR_OK) return st;
     if (part == 1 && c->pending_frame != frame_number) return BMFR_ERROR_INVALID_ARGUMENT;
     if (part != 1 && c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
+    DeviceGuard guard(c->device);
+    if (part != 1 && (st = reach_check(c, frame_number)) != BMFR_OK) return st;
     const hipStream_t s = as_stream(stream);
     const int cur = c->has_frame ? 1 - c->cur : 0;  // swap, bmfr.cpp:482-484
     bmfr::FusedArgs A = frame_args(c, in, m, off, frame_number, cur);
     const Params P = frame_params(c, frame_number);
     if (part != 2 && !bmfr::fused_supported(P)) return BMFR_ERROR_UNSUPPORTED;
+    // Profiling: 3 events of one slot per recorded frame; part 0 takes the
+    // slot, part 1 finishes it.
     hipEvent_t* ev = nullptr;
-    if (c->prof_capacity > 0 && frame_number % c->prof_stride == 0) {
-        const long n = part == 1 ? c->prof_count - 1 : c->prof_count;
-        ev = c->prof_events + 3 * (int)(n % c->prof_capacity);
-    }
-    if (part != 1 && ev) {
-        c->prof_frames[(int)(c->prof_count % c->prof_capacity)] = frame_number;
-        (void)hipEventRecord(ev[0], s);
+    if (part == 1) {
+        if (c->pending_prof_slot >= 0 && c->prof_capacity > 0)
+            ev = c->prof_events + 3 * (c->pending_prof_slot % c->prof_capacity);
+    } else if (c->prof_capacity > 0 && frame_number % c->prof_stride == 0) {
+        const int slot = (int)(c->prof_count % c->prof_capacity);
+        ev = c->prof_events + 3 * slot;
+        c->prof_frames[slot] = frame_number;
         ++c->prof_count;
+        (void)hipEventRecord(ev[0], s);
     }
     if (part == 2) {
         if (bmfr::fused_supported(P) && (st = hip_status(noise_for_frame(c, P, s, frame_number, &A.noise_table))))
@@ -548,9 +604,14 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
         // part 0 makes the table if needed, part 1 finds it in the cached range
         if ((st = hip_status(noise_for_frame(c, P, s, frame_number, &A.noise_table))) != BMFR_OK) return st;
         if (part == 0) {
-            st = hip_status(bmfr::launch_fused_k1_blocks(block_rect(P, ix0, ix1, iy0, iy1), s, A));
+            // Before the exchange only the tile's own state is valid.
+            Params I = block_rect(P, ix0, ix1, iy0, iy1);
+            const bmfr_config& g = c->cfg;
+            I.vx0 = g.tile_x, I.vy0 = g.tile_y, I.vx1 = g.tile_x + g.tile_width, I.vy1 = g.tile_y + g.tile_height;
+            st = hip_status(bmfr::launch_fused_k1_blocks(I, s, A));
             if (st != BMFR_OK) return st;
             c->pending_frame = frame_number;
+            c->pending_prof_slot = ev ? (int)((c->prof_count - 1) % c->prof_capacity) : -1;
             return BMFR_OK;
         }
         // The border ring in one launch (an empty interior leaves the whole rectangle).
@@ -564,8 +625,10 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
         if (ev) (void)hipEventRecord(ev[1], s);
         if ((st = hip_status(bmfr::launch_fused_k2(P, s, A))) != BMFR_OK) return st;
         c->pending_frame = -1;
+        c->pending_prof_slot = -1;
     }
     if (ev) (void)hipEventRecord(ev[2], s);
+    if (c->reach_event) (void)hipEventRecord(c->reach_event, s);
     c->cur = cur;
     c->has_frame = true;
     return BMFR_OK;
@@ -586,6 +649,7 @@ bmfr_status bmfr_process_sequence(bmfr_ctx* c, void* stream, int count, const bm
         return BMFR_ERROR_INVALID_ARGUMENT;
     if (c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
     if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // tiles exchange a halo between frames
+    DeviceGuard guard(c->device);
     const hipStream_t s = as_stream(stream);
     const size_t out_bytes = c->sizes.region_bytes;
     const bool pipelined = bmfr::fused_supported(c->P);
@@ -719,6 +783,7 @@ bmfr_status bmfr_halo_copy(bmfr_ctx* c, void* stream, const int* rects, int n, v
                            size_t* bytes) {
     if (!c || n < 0 || (n > 0 && !rects) || n * 4 > bmfr::kMaxHaloSegs) return BMFR_ERROR_INVALID_ARGUMENT;
     if (!is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
+    DeviceGuard guard(c->device);
     const int i = c->cur;  // bmfr_state(previous = 0): the last frame's state
     struct {
         uint8_t* base;
@@ -750,13 +815,14 @@ bmfr_status bmfr_halo_copy(bmfr_ctx* c, void* stream, const int* rects, int n, v
 }
 
 bmfr_status bmfr_set_profiling_stride(bmfr_ctx* c, int stride) {
-    if (!c || stride <= 0) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (!c || stride <= 0 || c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
     c->prof_stride = stride;
     return BMFR_OK;
 }
 
 bmfr_status bmfr_set_profiling(bmfr_ctx* c, int enable, int capacity) {
-    if (!c || (enable && capacity <= 0)) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (!c || (enable && capacity <= 0) || c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
+    DeviceGuard guard(c->device);
     if (c->prof_events) {
         (void)hipDeviceSynchronize();
         for (int i = 0; i < 3 * c->prof_capacity; ++i) (void)hipEventDestroy(c->prof_events[i]);
@@ -780,6 +846,7 @@ bmfr_status bmfr_set_profiling(bmfr_ctx* c, int enable, int capacity) {
 
 bmfr_status bmfr_get_profile(bmfr_ctx* c, bmfr_frame_profile* out, int max_frames, int* count) {
     if (!c || !count || (max_frames > 0 && !out)) return BMFR_ERROR_INVALID_ARGUMENT;
+    DeviceGuard guard(c->device);
     const long have = c->prof_count < c->prof_capacity ? c->prof_count : c->prof_capacity;
     const long first = c->prof_count - have;
     int n = 0;
@@ -801,9 +868,22 @@ bmfr_status bmfr_get_profile(bmfr_ctx* c, bmfr_frame_profile* out, int max_frame
     return BMFR_OK;
 }
 
+bmfr_status bmfr_halo_status(bmfr_ctx* c, unsigned* overshoot) {
+    if (!c) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (overshoot) *overshoot = 0;
+    if (!c->reach_host) return BMFR_OK;  // untiled: the whole image is valid state
+    DeviceGuard guard(c->device);
+    const bmfr_status st = hip_status(hipEventSynchronize(c->reach_event));
+    if (st != BMFR_OK) return st;
+    const unsigned v = c->reach_host[0];
+    if (overshoot) *overshoot = v;
+    return v > 0 ? BMFR_ERROR_HALO_EXCEEDED : BMFR_OK;
+}
+
 bmfr_status bmfr_debug_stamps(const bmfr_ctx* c, unsigned long long* host, size_t count) {
     if (!c || !host) return BMFR_ERROR_INVALID_ARGUMENT;
     if (!c->stamps) return BMFR_ERROR_UNSUPPORTED;
+    DeviceGuard guard(c->device);
     const size_t n = (size_t)c->sizes.blocks * 8;
     return hip_status(hipMemcpy(host, c->stamps, (count < n ? count : n) * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost));

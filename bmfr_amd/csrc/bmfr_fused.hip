@@ -1,15 +1,16 @@
-// bmfr_fused.hip -- fused frame kernel K1 (one 256-thread work-group per
-// 32x32 block): accumulate_noisy_data -> min/max scaling -> Householder QR ->
-// back substitution -> weighted_sum -> temporal blend of the filtered colour
+// bmfr_fused.hip -- fused frame kernel K1 for f32 tmp_data
+// (USE_HALF_PRECISION_IN_TMP_DATA 0; half tmp_data runs the column-split K1
+// of bmfr_fused_cols.hip), one 256-thread work-group per 32x32 block:
+// accumulate_noisy_data -> min/max scaling -> Householder QR -> back
+// substitution -> weighted_sum -> temporal blend of the filtered colour
 // (bmfr.cl:287-849).  Tone mapping and TAA follow in K2 (bmfr_kernels.hip).
 //
 // Work decomposition: thread t owns rows t + 256*s (s = 0..3) of the
 // block's design matrix -- exactly the rows upstream's fitter work-item t
 // touches (bmfr.cl:516-563) -- so per-thread partial sums and the
 // 256 -> 64 -> 8 -> 1 reduction tree (bmfr.cl:25-87) are reproduced in
-// upstream's association.  The matrix stays in VGPRs as packed halves (the
-// values upstream round-trips through tmp_data are halves anyway) or f32, so
-// tmp_data never touches HBM.  Every arithmetic step is upstream's, rounded
+// upstream's association.  The matrix stays in VGPRs (f32), so tmp_data
+// never touches HBM.  Every arithmetic step is upstream's, rounded
 // the same way; parity: tests/test_gpu_parity.py (bit-exact vs the stage
 // kernels and the reference kernels).
 //
@@ -26,7 +27,7 @@ namespace bmfr {
 constexpr int kThreads = 256;
 constexpr int kS64Stride = 72;  // 64 + 8: conflict-free transposed reads
 
-// f32 matrix with the HalfMatrix interface (USE_HALF_PRECISION_IN_TMP_DATA 0).
+// The f32 design matrix, rows t + 256 s of every column.
 template <int B, int N>
 struct FloatRows {
     float v[B][N];
@@ -37,19 +38,6 @@ struct FloatRows {
         for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[f][i]));
     }
 };
-template <int B, int N>
-struct HalfRows {
-    h2 v[B][N / 2];
-    __device__ __forceinline__ float get(int f, int j) const { return (float)v[f][j >> 1][j & 1]; }
-    __device__ __forceinline__ void set(int f, int j, float x) { v[f][j >> 1][j & 1] = (_Float16)x; }
-    __device__ __forceinline__ void fence(int f) {
-#pragma unroll
-        for (int i = 0; i < N / 2; ++i) asm volatile("" : "+v"(v[f][i]));
-    }
-};
-
-template <int B, bool HALF>
-using Rows = typename std::conditional<HALF, HalfRows<B, kSubs>, FloatRows<B, kSubs>>::type;
 
 // LDS of one block.
 template <int B>
@@ -296,41 +284,28 @@ __device__ __forceinline__ void back_substitute(K1Lds<B>& L, int t) {
     if (x < B - 3) L.weights[x * 3 + ch] = R[((RE - 1) * RE + x) * 3 + ch];
 }
 
-#ifndef BMFR_K1_WAVES
-#define BMFR_K1_WAVES 1  // minimum waves per SIMD requested from the register allocator
-#endif
-template <int NS, int FS, bool HALF, bool TONE, class IN>
-__global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, NoisyInputs in, Camera cam, int frame,
-                                                    const float* __restrict__ albedo,
-                                                    float* __restrict__ tone_out,
-                                                    const float* __restrict__ acc_prev,
-                                                    float* __restrict__ noisy_out,
-                                                    uint8_t* __restrict__ spp_out,
-                                                    float2* __restrict__ prev_pixel_out,
-                                                    float* __restrict__ acc_out,
-                                                    const double* __restrict__ noise,
-                                                    unsigned long long* __restrict__ stamps) {
+template <int NS, int FS, class IN>
+__global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
     constexpr int B = NS + FS + 3;
     __shared__ K1Lds<B> L;
     const int t = threadIdx.x;
-#ifdef BMFR_NO_XCD_SWIZZLE
-    const int g = blockIdx.x;
-#else
     const int g = xcd_swizzle(blockIdx.x, gridDim.x);
-#endif
+    const int frame = A.frame;
+    const NoisyInputs& in = A.in;
     // Diagnostic build only (-DBMFR_STAMPS): per-block phase timestamps.
 #ifdef BMFR_STAMPS
 #define BMFR_STAMP(k) \
-    if (t == 0 && stamps) stamps[(size_t)g * 8 + (k)] = __builtin_amdgcn_s_memtime()
+    if (t == 0 && A.stamps) A.stamps[(size_t)g * 8 + (k)] = __builtin_amdgcn_s_memtime()
 #else
-#define BMFR_STAMP(k) (void)stamps
+#define BMFR_STAMP(k) (void)0
 #endif
     BMFR_STAMP(0);
     int bx, by;
     k1_block(P, g, bx, by);
 
     // ---- accumulate_noisy_data (bmfr.cl:310-484) for rows t + 256s ----
-    Rows<B, HALF> A;
+    FloatRows<B, kSubs> M;
+    int over = 0;
     uint32_t state = 0;  // per s: owner (bit 0), accept bits (1-4), spp (8-15) -> 16 bits each ...
     uint32_t state_hi = 0;
     NoisyCur cur[kSubs];  // current-frame loads of all four rows go out first
@@ -339,28 +314,26 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
         cur[s] = noisy_load_current<IN>(P, in, bx * kEdge + (t & (kEdge - 1)), by * kEdge + (t >> 5) + 8 * s, frame);
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {
-        const NoisyItem it = noisy_item_spec<false, IN>(P, in, cam, cur[s], frame);
+        const NoisyItem it = noisy_item_spec<false, IN>(P, in, A.cam, cur[s], frame);
+        over = max(over, it.over);
 #pragma unroll
         for (int f = 0; f < B; ++f) {
             float v;
             if (f < B - 3) v = feature_value(f, it.n, it.p);
             else v = f == B - 3 ? it.color.x : (f == B - 2 ? it.color.y : it.color.z);
             if (__builtin_isnan(v)) v = 0.0f;           // bmfr.cl:468-469
-            if (HALF) v = fmaxf(fminf(v, 65504.f), -65504.f);  // bmfr.cl:471-473
-            A.set(f, s, v);
+            M.set(f, s, v);
         }
         const uint32_t bits = (uint32_t)it.owner | ((uint32_t)it.accept << 1) | ((uint32_t)it.spp << 8);
         if (s < 2) state |= bits << (16 * s);
         else state_hi |= bits << (16 * (s - 2));
         if (it.owner) {
-            st3(noisy_out, it.lin, it.color);
-            spp_out[it.lin] = it.spp;
-            prev_pixel_out[it.lin] = make_float2(it.pfx, it.pfy);
+            st3(A.noisy_out, it.lin, it.color);
+            A.spp_out[it.lin] = it.spp;
+            A.prev_pixel_out[it.lin] = make_float2(it.pfx, it.pfy);
         }
-#ifdef BMFR_P1_SERIAL
-        __builtin_amdgcn_sched_barrier(0);
-#endif
     }
+    report_reach(P, A.reach, over);
 
     BMFR_STAMP(1);
     // ---- scale the position features to the block's [min, max] (bmfr.cl:510-542) ----
@@ -371,8 +344,8 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
             float hi = -INFINITY, lo = INFINITY;
 #pragma unroll
             for (int s = 0; s < kSubs; ++s) {
-                hi = fmaxf(A.get(NS + f, s), hi);
-                lo = fminf(A.get(NS + f, s), lo);
+                hi = fmaxf(M.get(NS + f, s), hi);
+                lo = fminf(M.get(NS + f, s), lo);
             }
             mm[f] = hi;
             mm[FS + f] = lo;
@@ -391,20 +364,20 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
             }
 #pragma unroll
             for (int s = 0; s < kSubs; ++s) {
-                const float v = A.get(NS + f, s) - bmin;
-                A.set(NS + f, s, divide ? div_by_recip(v, d, rcp) : v);
+                const float v = M.get(NS + f, s) - bmin;
+                M.set(NS + f, s, divide ? div_by_recip(v, d, rcp) : v);
             }
         }
     }
 
     BMFR_STAMP(2);
     // ---- Householder QR over the feature columns (bmfr.cl:544-656) ----
-    qr_columns<B>(A, L, t, noise, P.noise2, std::make_integer_sequence<int, B - 3>{});
+    qr_columns<B>(M, L, t, A.noise, P.noise2, std::make_integer_sequence<int, B - 3>{});
     // Right-hand side: rows 0..B-4 of the colour columns, which the colour
     // columns' own Householder steps never touch (bmfr.cl:550, 596-600, 606).
     if (t < B - 3) {
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) L.R[((B - 3) * (B - 2) + t) * 3 + ch] = A.get(B - 3 + ch, 0);
+        for (int ch = 0; ch < 3; ++ch) L.R[((B - 3) * (B - 2) + t) * 3 + ch] = M.get(B - 3 + ch, 0);
     }
     __syncthreads();
     BMFR_STAMP(3);
@@ -418,7 +391,7 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
     const int2 off = kBlockOffsets[frame & 15];
     // All loads of the four rows first (normal, position, reprojection), then
     // the colours and the previous accumulation's taps.
-    f3 n[kSubs], pos[kSubs], alb[kSubs];
+    f3 n[kSubs], pos[kSubs];
     float2 pp[kSubs];
     long lin[kSubs];
     uint32_t bits[kSubs];
@@ -431,8 +404,7 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
         lin[s] = pix(P, (bits[s] & 1u) ? px : P.ox, (bits[s] & 1u) ? py : P.oy);
         n[s] = ld3in<IN>(in.n_cur, lin[s]);
         pos[s] = ld3in<IN>(in.p_cur, lin[s]);
-        pp[s] = prev_pixel_out[lin[s]];
-        if (TONE) alb[s] = ld3in<IN>(albedo, lin[s]);
+        pp[s] = A.prev_pixel_out[lin[s]];
     }
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {
@@ -455,9 +427,8 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
             c.y = c.y < 0.f ? 0.f : c.y;
             c.z = c.z < 0.f ? 0.f : c.z;
             const f3 acc = blend_filtered(P, c, pp[s].x, pp[s].y, (uint8_t)((bits[s] >> 1) & 15u),
-                                          (uint8_t)(bits[s] >> 8), acc_prev, frame);
-            st3(acc_out, lin[s], acc);
-            if (TONE) st3(tone_out, lin[s], tone_map(P, alb[s], acc));  // bmfr.cl:851-856
+                                          (uint8_t)(bits[s] >> 8), A.acc_prev, frame);
+            st3(A.acc_out, lin[s], acc);
         }
     }
 #ifdef BMFR_STAMPS
@@ -468,32 +439,20 @@ __global__ __launch_bounds__(kThreads, BMFR_K1_WAVES) void k_fused(Params P, Noi
 }
 
 bool fused_supported(const Params& P) {
-    if (P.fused_variant == 1 || P.not_scaled != 4 || (P.scaled != 6 && P.scaled != 9)) return false;
+    if (P.not_scaled != 4 || (P.scaled != 6 && P.scaled != 9)) return false;
     for (int f = 0; f < P.buffers - 3; ++f)
         if (P.codes[f] != f) return false;
     return true;
 }
 
-template <int NS, int FS, bool HALF, class IN>
+template <int FS, class IN>
 static void launch_k1(const Params& P, hipStream_t st, const FusedArgs& A) {
-    if (k1_tone_maps(P))
-        hipLaunchKernelGGL((k_fused<NS, FS, HALF, true, IN>), dim3(k1_blocks(P)), dim3(kThreads), 0, st, P,
-                           A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
-                           A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
-    else
-        hipLaunchKernelGGL((k_fused<NS, FS, HALF, false, IN>), dim3(k1_blocks(P)), dim3(kThreads), 0, st, P,
-                           A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
-                           A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
-}
-
-template <int FS, bool HALF>
-static void launch_k1_in(const Params& P, hipStream_t st, const FusedArgs& A) {
-    P.input_half ? launch_k1<4, FS, HALF, _Float16>(P, st, A) : launch_k1<4, FS, HALF, float>(P, st, A);
+    hipLaunchKernelGGL((k_fused<4, FS, IN>), dim3(k1_blocks(P)), dim3(kThreads), 0, st, P, k1_args(A));
 }
 
 hipError_t launch_fused_k1(const Params& P, hipStream_t st, const FusedArgs& A) {
-    if (P.scaled == 6) P.half_tmp ? launch_k1_in<6, true>(P, st, A) : launch_k1_in<6, false>(P, st, A);
-    else P.half_tmp ? launch_k1_in<9, true>(P, st, A) : launch_k1_in<9, false>(P, st, A);
+    if (P.scaled == 6) P.input_half ? launch_k1<6, _Float16>(P, st, A) : launch_k1<6, float>(P, st, A);
+    else P.input_half ? launch_k1<9, _Float16>(P, st, A) : launch_k1<9, float>(P, st, A);
     return hipGetLastError();
 }
 

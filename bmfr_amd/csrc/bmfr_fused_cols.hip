@@ -35,33 +35,8 @@ namespace cols {
 
 constexpr int kThreads = 256;
 constexpr int kSlots = 16;    // rows per lane per column (row = lane + 64 j)
-#ifndef BMFR_STAGGER
-#define BMFR_STAGGER 24000  // cycles; 0 = off (+1.3 % K1 throughput measured at 16-24K)
-#endif
-#ifndef BMFR_PK_P3
-#define BMFR_PK_P3 1  // weighted sum over packed item pairs
-#endif
-#ifndef BMFR_M_SWIZZLE
-#define BMFR_M_SWIZZLE 1  // design matrix row slots XOR-swizzled in LDS (conflict-free phase-1 stores)
-#endif
-constexpr int kUStride = 20;  // floats per lane in a u buffer: 16 + 4 (conflict-free 16-byte reads)
-
-#ifndef BMFR_PARK_GLOBAL
-// Phase 1 -> 3 hand-over of the previous accumulated filtered colour
-// (bmfr.cl:786-842, read at the noisy accumulation's taps): 0 = parked in
-// LDS (12 KB per block); 1 = parked in the owner pixel of the output plane
-// acc_out itself, which phase 3 then overwrites (same thread, same address:
-// program order) -- no LDS, so 5 blocks/CU fit, but measured slower
-// (0.446 vs 0.434 ms at 4K, and 0.465 at 5 blocks/CU with the spills that
-// 96 VGPRs cost).
-#define BMFR_PARK_GLOBAL 0
-#endif
-#ifndef BMFR_P3_TAPS
-// 1: the filtered colour's taps are read in phase 3 instead (blend_filtered,
-// from the prev-frame pixel this thread stored in phase 1): no hand-over at
-// all, fewer phase-1 registers, one more dependent round trip in phase 3.
-#define BMFR_P3_TAPS 0
-#endif
+constexpr int kStagger = 24000;  // cycles between first-round work-group groups (k1_stagger)
+constexpr int kUStride = 20;     // floats per lane in a u buffer: 16 + 4 (conflict-free 16-byte reads)
 
 template <int B>
 struct Lds {
@@ -69,16 +44,11 @@ struct Lds {
         _Float16 M[B - 1][64 * kSlots];  // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
         float u[2][64 * kUStride];       // Householder vectors, double-buffered by column parity
     };
-#if !BMFR_PARK_GLOBAL && !BMFR_P3_TAPS
     float keep[4][3][kThreads];  // phase 1 -> 3: previous accumulated filtered colour per item
-#endif
     float piv[2][2];                    // |u|^2 and RN(1/|u|^2) of the published vector
     float R[(B - 2) * (B - 2) * 3];     // R[x][y][ch], x = column (as k_fused)
     float weights[(B - 3) * 3];
     float mm[3 * (B - 3)];              // per scaled feature: min, max, 1/(max-min)
-#ifdef BMFR_LDS_PAD
-    float pad[BMFR_LDS_PAD / 4];        // occupancy experiments only
-#endif
 };
 static_assert(sizeof(float) * 2 * 64 * kUStride <= sizeof(_Float16) * 12 * 64 * kSlots,
               "u buffers must fit in the matrix area (B >= 13)");
@@ -133,16 +103,11 @@ __device__ __forceinline__ float sub_h(h2 h, float q) {
 // reciprocal (exact for these operand ranges, tests/test_markstein.py);
 // non-finite or extreme operands take IEEE division (uniform branch).
 typedef float f2v __attribute__((ext_vector_type(2)));
-#ifndef BMFR_PK_UPDATE
-#define BMFR_PK_UPDATE 1  // column update on packed f32 pairs (v_pk_add/mul/fma_f32)
-#endif
-#if BMFR_PK_UPDATE
-// The same per-element operations as below, two rows per instruction: the
-// dot's four partial chains run as two packed pairs (chain m sums rows
-// j = m + 4 si in order si = 0..3, so rows 4si, 4si+1 of one step feed
-// chains 0, 1 together), and the quotients as packed Markstein steps.  Every
-// lane of a packed op rounds like the scalar op, so the results are the
-// scalar path's bit for bit.
+// Upstream's per-element operations, two rows per instruction: the dot's four
+// partial chains (chain m sums rows j = m + 4 si in order si = 0..3, so rows
+// 4si, 4si+1 of one step feed chains 0, 1 together) run as two packed pairs,
+// and the quotients as packed Markstein steps.  Every lane of a packed op
+// rounds like the scalar op.
 template <int c>
 __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
                                               int l) {
@@ -182,47 +147,6 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
         a[k] = __builtin_convertvector((f2v{sub_h<0>(a[k], q[k].x), sub_h<1>(a[k], q[k].y)}), h2);
     __builtin_amdgcn_sched_barrier(0);  // one column in flight: bounds the register footprint
 }
-#else
-template <int c>
-__device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
-                                              int l) {
-    float p[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        float s = 0.f;
-#pragma unroll
-        for (int si = 0; si < 4; ++si) {
-            const int j = m + 4 * si;
-            float pr = (j & 1) ? mul_h<1>(a[j >> 1], u[j]) : mul_h<0>(a[j >> 1], u[j]);
-            if (j == 0) pr = l >= c ? pr : 0.f;  // rows above the pivot: skipped (0.f + 0.f + ... is the same sum)
-            s = s + pr;
-        }
-        p[m] = s;
-    }
-    const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);  // (2u) dot == u (2 dot): same real product, one rounding
-    float q[kSlots];
-    if (fabsf(c2) < 0x1p100f && ulen2 >= 0x1p-100f && ulen2 < 0x1p100f) {
-#pragma unroll
-        for (int j = 0; j < kSlots; ++j) q[j] = div_by_recip(u[j] * c2, ulen2, recip);
-    } else {
-        float c2s = c2;  // opaque: keeps the products inside this (cold) branch
-        asm volatile("" : "+v"(c2s));
-#pragma unroll
-        for (int j = 0; j < kSlots; ++j) {
-            q[j] = (u[j] * c2s) / ulen2;
-            __builtin_amdgcn_sched_barrier(0);  // never taken in practice: keep it narrow
-        }
-    }
-    q[0] = l >= c ? q[0] : 0.f;  // x - (+0) == x: rows above the pivot keep their value
-#pragma unroll
-    for (int k = 0; k < kSlots / 2; ++k) {
-        const float n0 = sub_h<0>(a[k], q[2 * k]), n1 = sub_h<1>(a[k], q[2 * k + 1]);
-        a[k] = h2{(_Float16)n0, (_Float16)n1};
-    }
-    __builtin_amdgcn_sched_barrier(0);  // one column in flight: bounds the register footprint
-}
-
-#endif
 
 // Step 0: column 0 is FEATURE_BUFFERS[0] = 1.f, so u = (1 - 32, 1, 1, ...),
 // |u|^2 = 1984 and u*x = x exactly (see k_fused's qr_column<0>).  Noise is
@@ -314,22 +238,9 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B>& L, int l
     }
 }
 
-#ifndef BMFR_LDS_BARRIERS
-#define BMFR_LDS_BARRIERS 1
-#endif
 // The work-group shares data through LDS only, so its barriers need not
 // wait for its global loads and stores (__syncthreads() does).
-__device__ __forceinline__ void k1_barrier() {
-    if constexpr (BMFR_LDS_BARRIERS) lds_barrier();
-    else __syncthreads();
-}
-
-#ifndef BMFR_P3_EARLY
-#define BMFR_P3_EARLY 1  // phase-3 loads in flight across back substitution
-#endif
-#ifndef BMFR_PIVOT_PRIO
-#define BMFR_PIVOT_PRIO 0  // s_setprio while a wave computes and publishes the next pivot column
-#endif
+__device__ __forceinline__ void k1_barrier() { lds_barrier(); }
 
 // Wave W's part of the fit: columns c = W (mod 4), c >= 1 (column 0 is implicit).
 template <int W, int NS, int FS>
@@ -374,10 +285,8 @@ struct WaveFit {
                 const float ulen2 = L.piv[c & 1][0], recip = L.piv[c & 1][1];
                 if constexpr (publish) {
                     // the next pivot is every wave's critical path: issue it first
-                    if (BMFR_PIVOT_PRIO) __builtin_amdgcn_s_setprio(BMFR_PIVOT_PRIO);
                     update_column<c>(a[nxt >> 2], u, ulen2, recip, l);
                     publish_pivot<nxt, B>(a[nxt >> 2], L, l);
-                    if (BMFR_PIVOT_PRIO) __builtin_amdgcn_s_setprio(0);
                 }
                 sfor<NSL>([&](auto K) {
                     constexpr int fb = W + 4 * decltype(K)::value;
@@ -403,19 +312,11 @@ struct WaveFit {
         sfor<NSL>([&](auto K) {
             constexpr int c = W + 4 * decltype(K)::value;
             if constexpr (owns(c)) {
-#if BMFR_M_SWIZZLE
                 // pair p of lane l's row slot sits at dword p ^ ((l >> 2) & 7) (see phase 1)
                 const uint32_t* src = reinterpret_cast<const uint32_t*>(&L.M[c - 1][l * kSlots]);
                 const int q = (l >> 2) & 7;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) a[c >> 2][i] = __builtin_bit_cast(h2, src[i ^ q]);
-#else
-                const uint4* src = reinterpret_cast<const uint4*>(&L.M[c - 1][l * kSlots]);
-                const uint4 lo = src[0], hi = src[1];
-                const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-#pragma unroll
-                for (int i = 0; i < 8; ++i) a[c >> 2][i] = __builtin_bit_cast(h2, w[i]);
-#endif
             }
         });
         k1_barrier();  // the u buffers alias M
@@ -496,26 +397,22 @@ __device__ __forceinline__ void back_substitute(Lds<B>& L, int t) {
     if (x < B - 3) L.weights[x * 3 + ch] = R[((RE - 1) * RE + x) * 3 + ch];
 }
 
-#ifndef BMFR_COLS_WAVES
-#define BMFR_COLS_WAVES 4  // minimum waves per SIMD requested from the register allocator (128 VGPRs: 4 WGs/CU)
-#endif
+constexpr int kColsWaves = 4;  // minimum waves per SIMD for the register allocator (128 VGPRs: 4 WGs/CU)
+constexpr int kBatch = 2;      // phase-1 items whose current-frame loads are issued together (4: > 128 VGPRs)
+
 // One K1 work-group (block g of the launch), on the LDS area L.
-template <int NS, int FS, class IN, bool TONE>
-__device__ __forceinline__ void k1_cols_body(const Params& P, const NoisyInputs& in, const Camera& cam, int frame,
-                                             const float* __restrict__ albedo, float* __restrict__ tone_out,
-                                             const float* __restrict__ acc_prev, float* __restrict__ noisy_out,
-                                             uint8_t* __restrict__ spp_out, float2* __restrict__ prev_pixel_out,
-                                             float* __restrict__ acc_out, const double* __restrict__ noise,
-                                             unsigned long long* __restrict__ stamps, Lds<NS + FS + 3>& L, int g) {
+template <int NS, int FS, class IN>
+__device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, Lds<NS + FS + 3>& L, int g) {
     constexpr int B = NS + FS + 3;
     const int t = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int l = t & 63;
+    const int frame = A.frame;
 #ifdef BMFR_STAMPS
 #define BMFR_STAMP(k) \
-    if (t == 0 && stamps) stamps[(size_t)g * 8 + (k)] = __builtin_amdgcn_s_memtime()
+    if (t == 0 && A.stamps) A.stamps[(size_t)g * 8 + (k)] = __builtin_amdgcn_s_memtime()
 #else
-#define BMFR_STAMP(k) (void)stamps
+#define BMFR_STAMP(k) (void)0
 #endif
     BMFR_STAMP(0);
     int bx, by;
@@ -523,28 +420,22 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const NoisyInputs&
     const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
 
     // ---- accumulate_noisy_data (bmfr.cl:310-484), rows l + 64 (4w + i) ----
-#if defined(BMFR_P1_B16) && BMFR_M_SWIZZLE
-#error "BMFR_P1_B16 stores halves unswizzled: build it with -DBMFR_M_SWIZZLE=0"
-#endif
-    h2 pk[B];  // features of an item pair, packed for one 4-byte LDS store per column
+    h2 pk[B];            // features of an item pair, packed for one 4-byte LDS store per column
     uint32_t spps = 0;   // per item i, bits 8i..8i+7: its new spp
     uint32_t ibits = 0;  // per item i, bit i: owner; bit 4 + i: accepted taps with weight > 0
+    int over = 0;        // reprojection taps outside the valid state rectangle (tiled contexts)
     // The temporal part of accumulate_filtered_data is read at the noisy
-    // accumulation's taps (bmfr.cl:786-842) and parked for phase 3.
-#ifndef BMFR_P1_BATCH
-#define BMFR_P1_BATCH 2  // items whose current-frame loads are issued together (4: > 128 VGPRs)
-#endif
-    constexpr int PB = BMFR_P1_BATCH;
+    // accumulation's taps (bmfr.cl:786-842) and parked in LDS for phase 3.
 #pragma unroll
-    for (int i0 = 0; i0 < 4; i0 += PB) {
-        NoisyCur cur[PB];
+    for (int i0 = 0; i0 < 4; i0 += kBatch) {
+        NoisyCur cur[kBatch];
 #pragma unroll
-        for (int k = 0; k < PB; ++k)
-            cur[k] = noisy_load_current<IN>(P, in, bx * kEdge + lx, by * kEdge + ly + 2 * (i0 + k), frame);
+        for (int k = 0; k < kBatch; ++k)
+            cur[k] = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly + 2 * (i0 + k), frame);
 #pragma unroll
-        for (int k = 0; k < PB; ++k) {
+        for (int k = 0; k < kBatch; ++k) {
             const int i = i0 + k;
-            const NoisyItem it = noisy_item_spec<!BMFR_P3_TAPS, IN>(P, in, cam, cur[k], frame, acc_prev);
+            const NoisyItem it = noisy_item_spec<true, IN>(P, A.in, A.cam, cur[k], frame, A.acc_prev);
 #pragma unroll
             for (int f = 1; f < B; ++f) {
                 float v;
@@ -552,42 +443,29 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const NoisyInputs&
                 else v = f == B - 3 ? it.color.x : (f == B - 2 ? it.color.y : it.color.z);
                 if (__builtin_isnan(v)) v = 0.0f;              // bmfr.cl:468-469
                 v = fmaxf(fminf(v, 65504.f), -65504.f);         // bmfr.cl:471-473
-#ifdef BMFR_P1_B16
-                L.M[f - 1][l * kSlots + 4 * w + i] = (_Float16)v;
-#else
                 pk[f][i & 1] = (_Float16)v;
-#endif
             }
             spps |= (uint32_t)it.spp << (8 * i);
             ibits |= ((uint32_t)it.owner << i) | ((uint32_t)it.prev_f_divided << (4 + i));
-#if BMFR_P3_TAPS
-            ibits |= (uint32_t)it.accept << (8 + 4 * i);  // accepted taps (bmfr.cl:380-404)
-#elif BMFR_PARK_GLOBAL
-            if (it.owner) st3(acc_out, it.lin, it.prev_f);
-#else
+            over = max(over, it.over);
             L.keep[i][0][t] = it.prev_f.x;
             L.keep[i][1][t] = it.prev_f.y;
             L.keep[i][2][t] = it.prev_f.z;
-#endif
             if (it.owner) {
-                st3(noisy_out, it.lin, it.color);
-                spp_out[it.lin] = it.spp;
-                prev_pixel_out[it.lin] = make_float2(it.pfx, it.pfy);
+                st3(A.noisy_out, it.lin, it.color);
+                A.spp_out[it.lin] = it.spp;
+                A.prev_pixel_out[it.lin] = make_float2(it.pfx, it.pfy);
             }
-#ifndef BMFR_P1_B16
             if (i & 1) {  // rows j = 4w + i - 1, 4w + i: adjacent halves of lane l's row slot
                 // (pair 2w + i/2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)
-                const int pair = BMFR_M_SWIZZLE ? (2 * w + i / 2) ^ ((l >> 2) & 7) : 2 * w + i / 2;
+                const int pair = (2 * w + i / 2) ^ ((l >> 2) & 7);
 #pragma unroll
                 for (int f = 1; f < B; ++f)
                     *reinterpret_cast<uint32_t*>(&L.M[f - 1][l * kSlots + 2 * pair]) = __builtin_bit_cast(uint32_t, pk[f]);
             }
-#endif
-#ifdef BMFR_P1_SERIAL
-            __builtin_amdgcn_sched_barrier(0);
-#endif
         }
     }
+    report_reach(P, A.reach, over);
     k1_barrier();  // matrix in LDS; phase 1's global stores drain in the background
     BMFR_STAMP(1);
     BMFR_STAMP(2);  // scaling runs inside the per-wave fit
@@ -595,10 +473,10 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const NoisyInputs&
     // ---- fit: min/max scaling, Householder QR, right-hand side ----
     const auto park = [] {};
     switch (w) {
-        case 0: WaveFit<0, NS, FS>::run(L, l, noise, P.noise2, park); break;
-        case 1: WaveFit<1, NS, FS>::run(L, l, noise, P.noise2, park); break;
-        case 2: WaveFit<2, NS, FS>::run(L, l, noise, P.noise2, park); break;
-        default: WaveFit<3, NS, FS>::run(L, l, noise, P.noise2, park); break;
+        case 0: WaveFit<0, NS, FS>::run(L, l, A.noise, P.noise2, park); break;
+        case 1: WaveFit<1, NS, FS>::run(L, l, A.noise, P.noise2, park); break;
+        case 2: WaveFit<2, NS, FS>::run(L, l, A.noise, P.noise2, park); break;
+        default: WaveFit<3, NS, FS>::run(L, l, A.noise, P.noise2, park); break;
     }
     // Phase 3's loads (normal and position of the four items, bmfr.cl:725-729)
     // go out now: they land while wave 0 back-substitutes and the others wait.
@@ -612,35 +490,19 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const NoisyInputs&
         const int px = bx * kEdge + (l3 & (kEdge - 1)) - kEdge / 2 + off.x;
         const int py = by * kEdge + (l3 >> 5) + 8 * w + 2 * i - kEdge / 2 + off.y;
         lin[i] = pix(P, (ibits & (1u << i)) ? px : P.ox, (ibits & (1u << i)) ? py : P.oy);  // margins: a valid pixel, skipped below
-        nrm[i] = ld3in<IN>(in.n_cur, lin[i]);
-        wp[i] = ld3in<IN>(in.p_cur, lin[i]);
+        nrm[i] = ld3in<IN>(A.in.n_cur, lin[i]);
+        wp[i] = ld3in<IN>(A.in.p_cur, lin[i]);
     }
-#if BMFR_P3_EARLY
     k1_barrier();  // R complete (LDS); with LDS-only barriers the loads above stay in flight
     BMFR_STAMP(3);
     back_substitute<B>(L, t);
     k1_barrier();  // weights complete
-#else
-    __syncthreads();
-    BMFR_STAMP(3);
-    back_substitute<B>(L, t);
-    __syncthreads();
-#endif
     BMFR_STAMP(4);
 
     // ---- weighted_sum (bmfr.cl:717-750) + temporal blend (bmfr.cl:778-849) ----
-#if BMFR_PARK_GLOBAL
-    f3 parked[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        if (ibits & (1u << i)) parked[i] = ld3(acc_out, lin[i]);  // this thread's phase-1 store
-#endif
     // Features outer, items inner: each weight / min-max is live for one
-    // feature only.  Every item still accumulates in feature order.
-    f3 c[4];
-#if BMFR_PK_P3
-    // Items (0, 1) and (2, 3) as packed f32 pairs: every lane rounds as the
-    // scalar sequence below.
+    // feature only.  Items (0, 1) and (2, 3) as packed f32 pairs: every lane
+    // rounds as upstream's scalar sequence, each item in feature order.
     f2v cp[2][3];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -672,61 +534,21 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const NoisyInputs&
         __builtin_amdgcn_sched_barrier(0);  // one feature's weights live at a time
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-        for (int k = 0; k < 2; ++k) c[2 * h + k] = f3{cp[h][0][k], cp[h][1][k], cp[h][2][k]};
-#else
-#pragma unroll
-    for (int i = 0; i < 4; ++i) c[i] = f3{0.f, 0.f, 0.f};
-#pragma unroll
-    for (int f = 0; f < B - 3; ++f) {
-        const float w0 = L.weights[3 * f], w1 = L.weights[3 * f + 1], w2 = L.weights[3 * f + 2];
-        float bmin = 0.f, d = 0.f, rcp = 0.f;
-        if (f >= NS) {
-            bmin = L.mm[3 * (f - NS)];
-            d = L.mm[3 * (f - NS) + 1] - bmin;
-            rcp = L.mm[3 * (f - NS) + 2];
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float v = feature_value(f, nrm[i], wp[i]);
-            if (f >= NS) {
-                v = v - bmin;
-                if (fabsf(d) > 1.0f) v = div_by_recip(v, d, rcp);
-            }
-            c[i].x = c[i].x + w0 * v;
-            c[i].y = c[i].y + w1 * v;
-            c[i].z = c[i].z + w2 * v;
-        }
-        __builtin_amdgcn_sched_barrier(0);  // one feature's weights live at a time
-    }
-#endif
-#pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (ibits & (1u << i)) {
-            f3 ci = c[i];
+            f3 ci{cp[i >> 1][0][i & 1], cp[i >> 1][1][i & 1], cp[i >> 1][2][i & 1]};
             ci.x = ci.x < 0.f ? 0.f : ci.x;
             ci.y = ci.y < 0.f ? 0.f : ci.y;
             ci.z = ci.z < 0.f ? 0.f : ci.z;
-#if BMFR_P3_TAPS
-            const float2 pf = prev_pixel_out[lin[i]];  // this thread's phase-1 store
-            const f3 acc = blend_filtered(P, ci, pf.x, pf.y, (uint8_t)((ibits >> (8 + 4 * i)) & 15u),
-                                          (uint8_t)((spps >> (8 * i)) & 255u), acc_prev, frame);
-#else
             // bmfr.cl:834-849: alpha from the current spp when the taps carried weight
             const float alpha = (ibits & (1u << (4 + i)))
                                     ? fmaxf(1.f / (float)((spps >> (8 * i)) & 255u), P.second_blend_alpha)
                                     : 1.f;
             const float beta = 1.f - alpha;
-#if BMFR_PARK_GLOBAL
-            const f3 prev = parked[i];
-#else
             const int t3 = l3 + 64 * w;
             const f3 prev{L.keep[i][0][t3], L.keep[i][1][t3], L.keep[i][2][t3]};
-#endif
             const f3 acc{alpha * ci.x + beta * prev.x, alpha * ci.y + beta * prev.y, alpha * ci.z + beta * prev.z};
-#endif
-            st3(acc_out, lin[i], acc);
-            if constexpr (TONE) st3(tone_out, lin[i], tone_map(P, ld3in<IN>(albedo, lin[i]), acc));  // bmfr.cl:851-856
+            st3(A.acc_out, lin[i], acc);
         }
     }
 #ifdef BMFR_STAMPS
@@ -736,39 +558,22 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const NoisyInputs&
 #undef BMFR_STAMP
 }
 
-// First round of work-groups: start the k-th group of 256 k * BMFR_STAGGER
+// First round of work-groups: start the k-th group of 256 k * kStagger
 // cycles late, so the four work-groups sharing a CU do not run their
 // memory-bound phase 1 and VALU-bound fit in lockstep (large launches only,
 // not a tile's border ring).
 __device__ __forceinline__ void k1_stagger(int b, int n) {
-#if BMFR_STAGGER
     if (b < 4 * 256 && n >= 8 * 256) {
-        const int k = ((b >> 8) & 3) * (BMFR_STAGGER / 8000);
+        const int k = ((b >> 8) & 3) * (kStagger / 8000);
         for (int s = 0; s < k; ++s) __builtin_amdgcn_s_sleep(125);
     }
-#endif
 }
 
-template <int NS, int FS, class IN, bool TONE>
-__global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params P, NoisyInputs in, Camera cam, int frame,
-                                                          const float* __restrict__ albedo,
-                                                          float* __restrict__ tone_out,
-                                                          const float* __restrict__ acc_prev,
-                                                          float* __restrict__ noisy_out,
-                                                          uint8_t* __restrict__ spp_out,
-                                                          float2* __restrict__ prev_pixel_out,
-                                                          float* __restrict__ acc_out,
-                                                          const double* __restrict__ noise,
-                                                          unsigned long long* __restrict__ stamps) {
+template <int NS, int FS, class IN>
+__global__ __launch_bounds__(kThreads, kColsWaves) void k_fused_cols(Params P, K1Args A) {
     __shared__ Lds<NS + FS + 3> L;
     k1_stagger(blockIdx.x, gridDim.x);
-#ifdef BMFR_NO_XCD_SWIZZLE
-    const int g = blockIdx.x;
-#else
-    const int g = xcd_swizzle(blockIdx.x, gridDim.x);
-#endif
-    k1_cols_body<NS, FS, IN, TONE>(P, in, cam, frame, albedo, tone_out, acc_prev, noisy_out, spp_out, prev_pixel_out,
-                                   acc_out, noise, stamps, L, g);
+    k1_cols_body<NS, FS, IN>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
 }
 
 // K1 of frame f and K2 (64 x kSeqTaaH tiles) of frame f - 1 in one launch:
@@ -779,14 +584,8 @@ __global__ __launch_bounds__(kThreads, BMFR_COLS_WAVES) void k_fused_cols(Params
 // of f does not write (double-buffered), and frame f - 2's TAA output.
 constexpr int kSeqTaaH = 8;
 template <int NS, int FS, class IN>
-__global__ __launch_bounds__(kThreads, 4) void k_fused_cols_taa(Params P, NoisyInputs in, Camera cam, int frame,
-                                                                const float* __restrict__ acc_prev,
-                                                                float* __restrict__ noisy_out,
-                                                                uint8_t* __restrict__ spp_out,
-                                                                float2* __restrict__ prev_pixel_out,
-                                                                float* __restrict__ acc_out,
-                                                                const double* __restrict__ noise, Params P2,
-                                                                TaaArgs T, int nk1, int nk1p) {
+__global__ __launch_bounds__(kThreads, 4) void k_fused_cols_taa(Params P, K1Args A, Params P2, TaaArgs T, int nk1,
+                                                                int nk1p) {
     constexpr int HW = 64 + 2, N = HW * (kSeqTaaH + 2);
     __shared__ union {
         Lds<NS + FS + 3> k1;
@@ -799,38 +598,26 @@ __global__ __launch_bounds__(kThreads, 4) void k_fused_cols_taa(Params P, NoisyI
     const int b = blockIdx.x;
     if (b < nk1) {
         k1_stagger(b, nk1);
-        k1_cols_body<NS, FS, IN, false>(P, in, cam, frame, nullptr, nullptr, acc_prev, noisy_out, spp_out,
-                                        prev_pixel_out, acc_out, noise, nullptr, U.k1, xcd_swizzle(b, nk1));
+        k1_cols_body<NS, FS, IN>(P, A, U.k1, xcd_swizzle(b, nk1));
     } else if (b >= nk1p) {
         const int gx = (P2.tx1 - P2.tx0 + 63) / 64, n2 = (int)gridDim.x - nk1p;
         const int gi = xcd_swizzle(b - nk1p, n2);
-        taa_tile<true, IN, kSeqTaaH>(P2, T, P2.tx0 + (gi % gx) * 64, P2.ty0 + (gi / gx) * kSeqTaaH, U.k2.Y, U.k2.sE,
-                                     U.k2.sRP);
+        taa_tile<IN, kSeqTaaH>(P2, T, P2.tx0 + (gi % gx) * 64, P2.ty0 + (gi / gx) * kSeqTaaH, U.k2.Y, U.k2.sE,
+                               U.k2.sRP);
     }
 }
 
 }  // namespace cols
 
-bool fused_cols_supported(const Params& P) {
-    return P.half_tmp && (P.fused_variant == 0 || P.fused_variant == 4 || P.fused_variant == 5) &&
-           fused_supported(P);
-}
+bool fused_cols_supported(const Params& P) { return P.half_tmp && fused_supported(P); }
 
 template <int FS, class IN>
 static void launch_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
-    if (k1_tone_maps(P))
-        hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, true>), dim3(k1_blocks(P)), dim3(cols::kThreads), 0, st, P,
-                           A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
-                           A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
-    else
-        hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, false>), dim3(k1_blocks(P)), dim3(cols::kThreads), 0, st,
-                           P, A.in, A.cam, A.frame, A.albedo, A.tone_out, A.acc_prev, A.noisy_out, A.spp_out,
-                           A.prev_pixel_out, A.acc_out, A.noise_table, A.stamps);
+    hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN>), dim3(k1_blocks(P)), dim3(cols::kThreads), 0, st, P,
+                       k1_args(A));
 }
 
-bool seq_fused_supported(const Params& P) {
-    return fused_cols_supported(P) && P.fused_variant == 0 && P.ring == 0 && (P.scaled == 6 || P.scaled == 9);
-}
+bool seq_fused_supported(const Params& P) { return fused_cols_supported(P) && P.ring == 0; }
 
 template <int FS, class IN>
 static void launch_cols_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
@@ -838,13 +625,9 @@ static void launch_cols_taa(const Params& P, hipStream_t st, const FusedArgs* A,
     const int nk1 = A ? k1_blocks(P) : 0, nk1p = (nk1 + 7) & ~7;
     const int nk2 = A2 ? ((P2.tx1 - P2.tx0 + 63) / 64) * ((P2.ty1 - P2.ty0 + cols::kSeqTaaH - 1) / cols::kSeqTaaH) : 0;
     if (nk1 + nk2 == 0) return;
-    const FusedArgs& a = A ? *A : *A2;
-    const TaaArgs T = A2 ? TaaArgs{A2->acc_out, A2->albedo, A2->prev_pixel_out, A2->result_out, A2->result_prev,
-                                   A2->frame}
-                         : TaaArgs{};
+    const TaaArgs T = A2 ? taa_args(*A2) : TaaArgs{};
     hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN>), dim3(nk2 ? nk1p + nk2 : nk1), dim3(cols::kThreads), 0,
-                       st, A ? P : P2, a.in, a.cam, a.frame, a.acc_prev, a.noisy_out, a.spp_out, a.prev_pixel_out,
-                       a.acc_out, a.noise_table, A2 ? P2 : P, T, nk1, nk1p);
+                       st, A ? P : P2, k1_args(A ? *A : *A2), A2 ? P2 : P, T, nk1, nk1p);
 }
 
 hipError_t launch_fused_k1_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,

@@ -91,6 +91,7 @@ struct NoisyItem {
     f3 prev_f;
     float alpha_f;
     bool prev_f_divided;  // the tap weights summed to > 0 (alpha_f from spp)
+    int over;             // noisy_item_spec, P.check_reach: px by which an in-image tap leaves [vx0, vx1) x [vy0, vy1)
 };
 
 struct NoisyInputs {
@@ -286,6 +287,7 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
     o.prev_f = f3{0.f, 0.f, 0.f};
     o.alpha_f = 1.f;
     o.prev_f_divided = false;
+    o.over = 0;
     float tap_total = 0.f;
     if (frame > 0) {
         const float* M = cam.m;
@@ -308,6 +310,12 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
         const float fx = pfx - flx, fy = pfy - fly;
         const float omx = 1.f - fx, omy = 1.f - fy;
         const float wts[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
+        if (P.check_reach) {  // the in-image taps span [x0, x1] x [y0, y1]
+            const int x0 = max(ix, 0), x1 = min(ix + 1, P.width - 1);
+            const int y0 = max(iy, 0), y1 = min(iy + 1, P.height - 1);
+            if (x0 <= x1 && y0 <= y1)
+                o.over = max(max(max(P.vx0 - x0, x1 - (P.vx1 - 1)), max(P.vy0 - y0, y1 - (P.vy1 - 1))), 0);
+        }
         f3 pp[4], pn[4], pc[4], pa[4];
         float sp[4];
         bool inb[4];
@@ -369,6 +377,13 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
     o.accept = accept;
     o.spp = new_spp;
     return o;
+}
+
+// One work-group's reprojection-reach report (tiled contexts): the lanes
+// whose taps left the valid state rectangle raise the context's maximum.
+__device__ __forceinline__ void report_reach(const Params& P, unsigned* reach, int over) {
+    if (P.check_reach && __builtin_amdgcn_ballot_w64(over > 0) != 0 && over > 0)
+        atomicMax(reach, (unsigned)over);
 }
 
 // tmp_data value of feature f for an item (bmfr.cl:448-473): NaN -> 0, and

@@ -12,7 +12,6 @@
 #include "bmfr_kernels.h"
 #include "bmfr_generic.h"
 #include "bmfr_launch.h"
-#include "bmfr_taa_tile.h"
 
 namespace bmfr {
 
@@ -107,63 +106,20 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
 }
 
 // --------------------------------------------------------- fused K2: TAA --
-// One 64 x kTaaH tile per 256-thread work-group (taa_tile, bmfr_taa_tile.h).
-// 64x16: 22 KB of LDS per work-group.
-#ifndef BMFR_K2_H  // tile height (multiple of 4)
-#define BMFR_K2_H 16
-#endif
-constexpr int kTaaW = 64, kTaaH = BMFR_K2_H;
-#ifndef BMFR_K2_WAVES  // minimum waves per SIMD the register allocation must allow
-#define BMFR_K2_WAVES 1
-#endif
-template <bool TONE, class IN>
-__global__ __launch_bounds__(256, BMFR_K2_WAVES) void k_fused_taa(Params P, const float* __restrict__ src,
-                                                                  const float* __restrict__ albedo,
-                                                                  const float2* __restrict__ prev_pixel,
-                                                                  float* __restrict__ result,
-                                                                  const float* __restrict__ prev_frame,
-                                                                  int frame) {
+// Tone map + TAA, one 64 x kTaaH tile per 256-thread work-group (taa_tile,
+// bmfr_taa_tile.h); 64x16: 22 KB of LDS per work-group.
+constexpr int kTaaW = 64, kTaaH = 16;
+template <class IN>
+__global__ __launch_bounds__(256) void k_fused_taa(Params P, TaaArgs T) {
     __shared__ float4 Y[(kTaaW + 2) * (kTaaH + 2)];  // YCoCg (+ pad): one 16-byte read per neighbour
-    __shared__ double sE[TONE ? kPowrENum : 1];
-    __shared__ double2 sRP[TONE ? kPowrRPNum : 1];
+    __shared__ double sE[kPowrENum];
+    __shared__ double2 sRP[kPowrRPNum];
     // Output tile of this launch (the whole image, or a multi-GPU tile whose
     // one-pixel halo lies inside the buffer region).
-#ifdef BMFR_NO_XCD_SWIZZLE
-    const int bxi = blockIdx.x, byi = blockIdx.y;
-#else
     const int gi = xcd_swizzle(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int bxi = gi % gridDim.x, byi = gi / gridDim.x;
-#endif
-    const TaaArgs T{src, albedo, prev_pixel, result, prev_frame, frame};
-    taa_tile<TONE, IN, kTaaH>(P, T, P.tx0 + bxi * kTaaW, P.ty0 + byi * kTaaH, Y, sE, sRP);
-}
-
-// ------------------------------------------------ stencil K2 (tonecols) --
-// TAA straight from K1's tone-mapped frame in global memory, one pixel per
-// thread over the output tile, no LDS: light enough (<= 64 VGPRs) to run
-// beside four resident K1 blocks per CU.  Border work-groups check every
-// neighbour (bmfr.cl:901); interior ones skip the tests.
-__global__ __launch_bounds__(256, 8) void k_taa_stencil(Params P, const float* __restrict__ tone,
-                                                     const float2* __restrict__ prev_pixel,
-                                                     float* __restrict__ result,
-                                                     const float* __restrict__ prev_frame, int frame) {
-    const int x0 = P.tx0 + blockIdx.x * blockDim.x, y0 = P.ty0 + blockIdx.y * blockDim.y;
-    const int x = x0 + threadIdx.x, y = y0 + threadIdx.y;
-    if (x >= P.tx1 || y >= P.ty1) return;
-    const long lin = pix(P, x, y);
-    const float2 pf = prev_pixel[lin];
-    f3 pc[4];
-    taa_load_taps(P, pf, prev_frame, pc);
-    const f3 me = ld3(tone, lin);
-    f3 nb[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k)  // out-of-image neighbours: a clamped in-image pixel, skipped by taa_resolve
-        nb[k] = k == 4 ? rgb_to_ycocg(me)
-                       : rgb_to_ycocg(ld3(tone, pix(P, min(max(x + k % 3 - 1, 0), P.width - 1),
-                                                    min(max(y + k / 3 - 1, 0), P.height - 1))));
-    const bool edge = x0 == 0 || y0 == 0 || x0 + (int)blockDim.x >= P.width || y0 + (int)blockDim.y >= P.height;
-    st3(result, lin, edge ? taa_resolve<true>(P, x, y, me, pf, nb, pc, frame)
-                          : taa_resolve<false>(P, x, y, me, pf, nb, pc, frame));
+    forward_reach(T);
+    taa_tile<IN, kTaaH>(P, T, P.tx0 + bxi * kTaaW, P.ty0 + byi * kTaaH, Y, sE, sRP);
 }
 
 // ------------------------------------------------------------ halo copy --
@@ -310,20 +266,8 @@ hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedAr
 
 hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A) {
     const dim3 grd((P.tx1 - P.tx0 + kTaaW - 1) / kTaaW, (P.ty1 - P.ty0 + kTaaH - 1) / kTaaH);
-    if (k2_stencil(P)) {
-        const dim3 blk(64, 4);
-        const dim3 g((P.tx1 - P.tx0 + 63) / 64, (P.ty1 - P.ty0 + 3) / 4);
-        hipLaunchKernelGGL(k_taa_stencil, g, blk, 0, st, P, A.tone_out, A.prev_pixel_out, A.result_out,
-                           A.result_prev, A.frame);
-    } else if (k1_tone_maps(P))
-        hipLaunchKernelGGL((k_fused_taa<false, float>), grd, dim3(256), 0, st, P, A.tone_out, A.albedo,
-                           A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
-    else if (P.input_half)
-        hipLaunchKernelGGL((k_fused_taa<true, _Float16>), grd, dim3(256), 0, st, P, A.acc_out, A.albedo,
-                           A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
-    else
-        hipLaunchKernelGGL((k_fused_taa<true, float>), grd, dim3(256), 0, st, P, A.acc_out, A.albedo,
-                           A.prev_pixel_out, A.result_out, A.result_prev, A.frame);
+    if (P.input_half) hipLaunchKernelGGL((k_fused_taa<_Float16>), grd, dim3(256), 0, st, P, taa_args(A));
+    else hipLaunchKernelGGL((k_fused_taa<float>), grd, dim3(256), 0, st, P, taa_args(A));
     return hipGetLastError();
 }
 

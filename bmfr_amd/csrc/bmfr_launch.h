@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "bmfr_kernels.h"
+#include "bmfr_taa_tile.h"
 
 namespace bmfr {
 
@@ -36,27 +37,42 @@ struct FusedArgs {
     float* tone_out;
     float* result_out;
     double* noise_table;  // (B-4) * 1024 noise terms NOISE_AMOUNT*2*(rnd-0.5) in double, context-owned
+    unsigned* reach;      // tiled contexts: max overshoot (px) of reprojection taps past the valid state
+    unsigned* reach_host; // tiled contexts: page-locked report of it (see TaaArgs)
     unsigned long long* stamps;  // diagnostic build: 8 timestamps per block, or null
 };
+
+// Kernel arguments of the fused K1 (canonical feature lists).
+struct K1Args {
+    NoisyInputs in;
+    Camera cam;
+    int frame;
+    const float* acc_prev;
+    float* noisy_out;
+    uint8_t* spp_out;
+    float2* prev_pixel_out;
+    float* acc_out;
+    const double* noise;
+    unsigned* reach;
+    unsigned long long* stamps;
+};
+inline K1Args k1_args(const FusedArgs& A) {
+    return K1Args{A.in,      A.cam,          A.frame,          A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out,
+                  A.acc_out, A.noise_table,  A.reach,          A.stamps};
+}
+inline TaaArgs taa_args(const FusedArgs& A) {
+    return TaaArgs{A.acc_out, A.albedo, A.prev_pixel_out, A.result_out, A.result_prev, A.frame, A.reach,
+                   A.reach_host};
+}
 
 bool fitter_supported(int not_scaled, int scaled);
 // Work-groups of a K1 launch (the rectangle, or its ring).
 inline int k1_blocks(const Params& P) { return P.ring > 0 ? P.ring : P.nbx * P.nby; }
 bool fused_supported(const Params& P);
-// Where the canonical path tone-maps (bmfr.cl:851-856): in K2 for each tile
-// pixel + halo (default: K1 is latency-bound and its VALU is the critical
-// resource; measured 0.68 vs 0.74 ms/frame at 4K), or in K1 for each owned
-// pixel, writing a tone-mapped frame (BMFR_FUSED_KERNEL=k1tone).
-// BMFR_FUSED_KERNEL=tonecols: column-split K1 tone-maps its owned pixels
-// and K2 is a register-only stencil (k_taa_stencil: no LDS, <= 64 VGPRs) that
-// fits beside four resident K1 blocks on a CU (bmfr_process_sequence).
-// BMFR_FUSED_KERNEL=colstone: column-split K1 tone-maps, K2 = LDS TAA on its frame.
-inline bool k1_tone_maps(const Params& P) {
-    return P.fused_variant == 2 || P.fused_variant == 4 || P.fused_variant == 5;
-}
-inline bool k2_stencil(const Params& P) { return P.fused_variant == 4; }
+// The canonical path tone-maps in K2 (bmfr.cl:851-856), for each tile pixel
+// and its 1-px halo.  f32 tmp_data: row-split K1 (bmfr_fused.hip).
 hipError_t launch_fused_k1(const Params& P, hipStream_t st, const FusedArgs& A);
-// Column-split K1 (bmfr_fused_cols.hip): default for half tmp_data.
+// Column-split K1 (bmfr_fused_cols.hip): half tmp_data.
 bool fused_cols_supported(const Params& P);
 hipError_t launch_fused_k1_cols(const Params& P, hipStream_t st, const FusedArgs& A);
 

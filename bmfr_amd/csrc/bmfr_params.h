@@ -37,9 +37,6 @@ struct Params {
     int half_tmp;                 // USE_HALF_PRECISION_IN_TMP_DATA
     int input_half;               // bmfr_config.input_half: frame input planes are half3
     int library_powr;             // bmfr_config.library_powr: tone map with __ocml_powr_f32
-    int fused_variant;            // 0 = default, 1 = generic-feature K1, 2 = tone map in K1, 3 = row-split K1,
-                                  // 4 = tone map in K1 + stencil K2, 5 = tone map in column-split K1
-                                  // + LDS K2 (A/B diagnostics)
     // Buffer region (multi-GPU tiles): every plane of the fused path holds the
     // image pixels [ox, ox + stride) x [oy, oy + rows), row stride `stride`.
     // Untiled: 0, 0, width, height -- the reference's layout.
@@ -52,6 +49,13 @@ struct Params {
     // bmfr_process_frame_border), ring = their count.
     int ring, rx0, ry0, rx1, ry1;
     int tx0, ty0, tx1, ty1;
+    // Tiled contexts (check_reach = 1): the previous frame's state is valid
+    // only in [vx0, vx1) x [vy0, vy1) for this launch -- the tile before the
+    // halo exchange (interior blocks), the region after it.  K1 reports the
+    // largest distance by which an in-image reprojection tap (bmfr.cl:374-419)
+    // falls outside it (include/bmfr.h: BMFR_ERROR_HALO_EXCEEDED).
+    int check_reach;
+    int vx0, vy0, vx1, vy1;
 };
 
 // BLOCK_OFFSETS (bmfr.cl:267-285), host copy of the device table in

@@ -254,6 +254,14 @@ class Denoiser(_Context):
         self._call("bmfr_process_frame_border", noisy, normals, positions, albedo, prev_vp, jitter, frame,
                    prev_normals, prev_positions, stream, True)
 
+    def halo_status(self) -> int:
+        """Tiled contexts: waits for the last frame; the largest distance (px)
+        by which a frame since frame 0 reprojected past its valid state (0 =
+        none).  Raises BmfrError (status HALO_EXCEEDED) when it is > 0."""
+        v = C.c_uint()
+        check(self.lib.bmfr_halo_status(self.handle, C.byref(v)), "bmfr_halo_status")
+        return v.value
+
     def set_profiling(self, enable: bool, capacity: int = 4096, stride: int = 1) -> None:
         """stride: record only frames whose number is a multiple of it."""
         check(self.lib.bmfr_set_profiling_stride(self.handle, stride), "bmfr_set_profiling_stride")

@@ -33,7 +33,7 @@ extern "C" {
 #endif
 
 #define BMFR_VERSION_MAJOR 0
-#define BMFR_VERSION_MINOR 1
+#define BMFR_VERSION_MINOR 2
 
 #define BMFR_BLOCK_EDGE_LENGTH 32 /* bmfr.cpp:104; other sizes unsupported, as upstream */
 #define BMFR_MAX_FEATURES 16      /* NOT_SCALED + SCALED feature buffers */
@@ -44,7 +44,9 @@ typedef enum bmfr_status {
     BMFR_ERROR_UNSUPPORTED = 2,     /* e.g. a feature count with no compiled kernel */
     BMFR_ERROR_OUT_OF_MEMORY = 3,
     BMFR_ERROR_HIP = 4,             /* a HIP runtime call failed (see bmfr_last_hip_error) */
-    BMFR_ERROR_NO_DEVICE = 5
+    BMFR_ERROR_NO_DEVICE = 5,
+    BMFR_ERROR_HALO_EXCEEDED = 6    /* tiled context: a frame reprojected past the exchanged halo
+                                       (see tile_halo, bmfr_halo_status) */
 } bmfr_status;
 
 /* Feature buffer monomials.  The reference pastes C expressions into the
@@ -87,8 +89,15 @@ typedef struct bmfr_config {
      * planes (noisy_accumulated, spp, filtered_accumulated, result of
      * bmfr_state(previous = 0)) from the neighbouring tiles, which own those
      * pixels.  Exact for scene motion below tile_halo - 34 pixels per frame
-     * (32: blocks reaching past the tile, 2: TAA + bilinear taps).  Canonical
-     * feature lists, fused path only (the stage API rejects tiled contexts). */
+     * (32: blocks reaching past the tile, 2: TAA + bilinear taps); the
+     * reference reprojects to any pixel (bmfr.cl:343-356), so the kernels
+     * check it: a frame whose reprojection taps reach past the state that
+     * is valid for them (the tile before the halo exchange, the region after
+     * it) makes bmfr_halo_status -- and every later bmfr_process_frame* call
+     * until frame_number 0 starts a new sequence -- return
+     * BMFR_ERROR_HALO_EXCEEDED instead of diverging silently from the
+     * untiled frame.  Canonical feature lists, fused path only (the stage API
+     * rejects tiled contexts). */
     int tile_x, tile_y, tile_width, tile_height;
     int tile_halo;
     /* Input planes of bmfr_process_frame (noisy, normals, positions, albedo
@@ -243,6 +252,12 @@ bmfr_status bmfr_process_sequence(bmfr_ctx *ctx, void *stream, int count, const 
  * receives the packed size; buffer = NULL only computes it.  n <= 16. */
 bmfr_status bmfr_halo_copy(bmfr_ctx *ctx, void *stream, const int *rects, int n, void *buffer, int unpack,
     size_t *bytes);
+
+/* Tiled contexts: waits for the last enqueued frame and returns
+ * BMFR_ERROR_HALO_EXCEEDED if any frame since frame 0 read reprojection taps
+ * past its valid state (see tile_halo), BMFR_OK otherwise; *overshoot
+ * (nullable) receives the largest distance in pixels.  Untiled: BMFR_OK. */
+bmfr_status bmfr_halo_status(bmfr_ctx *ctx, unsigned *overshoot);
 
 /* Device pointer to the last processed frame's output (TAA result, float3,
  * W*H, the buffer the reference reads back at bmfr.cpp:479-480).  Valid until

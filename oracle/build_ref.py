@@ -25,7 +25,7 @@ import yaml
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
-from ref_configs import REF_CONFIGS, REF_MODES  # noqa: E402
+from ref_configs import FULL_REF_CONFIGS, REF_CONFIGS, REF_MODES  # noqa: E402
 
 CLANG = "/opt/rocm/lib/llvm/bin/clang"
 READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
@@ -58,7 +58,7 @@ def build(ref_dir: str, force: bool = False) -> list:
     os.makedirs(OUT, exist_ok=True)
     src = os.path.join(HERE, "ref_wrappers.cl")
     built = []
-    for name, cfg in REF_CONFIGS.items():
+    for name, cfg in {**REF_CONFIGS, **FULL_REF_CONFIGS}.items():
         for mode, flags in REF_MODES.items():
             hsaco = os.path.join(OUT, f"{name}_{mode}.hsaco")
             meta = os.path.join(OUT, f"{name}_{mode}.json")

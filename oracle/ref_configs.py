@@ -128,6 +128,21 @@ REF_CONFIGS = {
     )
 }
 
+# BASELINE.json's configurations at their own sizes (GPU tests only: the CPU
+# oracle is too slow there, so no golden .npz; tests/golden/fullsize_digests.json
+# keeps SHA-256 digests of the reference's outputs).  frames: how many frames
+# tests/test_gpu_reference_fullsize.py compares.
+FULL_REF_CONFIGS = {
+    c.name: c
+    for c in (
+        RefConfig("f1920x1080_h13", 1920, 1080, frames=17),              # config 2
+        RefConfig("f3840x2160_h13", 3840, 2160, frames=4),               # config 3 (reference default build)
+        RefConfig("f3840x2160_f13", 3840, 2160, half_tmp=0, frames=4),   # config 3, fp32 tmp_data
+        RefConfig("f3840x2160_h16", 3840, 2160, scaled=SCALED_THIRD_ORDER, frames=4),  # config 5 (3rd order)
+        RefConfig("f1280x720_h13", 1280, 720, frames=60),                # a whole 60-frame sequence
+    )
+}
+
 # Build modes of the reference: "strict" fixes the arithmetic OpenCL leaves to
 # the implementation (no contraction, correctly rounded / and sqrt) and is the
 # one the oracle is pinned to bit-for-bit; "default" is what bmfr.cpp's

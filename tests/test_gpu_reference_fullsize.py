@@ -1,0 +1,176 @@
+"""BASELINE.json's configurations pinned at their own sizes directly to the
+reference's own kernels (oracle/ref_configs.py FULL_REF_CONFIGS: 1920x1080
+for 17 frames, 3840x2160 with half / f32 tmp_data and the 3rd-order B = 16
+feature set, the half-input variant of config 5, and a whole 60-frame
+1280x720 sequence).
+
+Per frame, on the GPU:
+  REF     /root/reference/opencl/bmfr.cl compiled by oracle/build_ref.py
+          (strict build), launched with the reference's geometry (RefLoop)
+  STAGES  libbmfr's five stage kernels (library_powr = 1: the reference
+          kernel's own powr) -- every inter-stage buffer bit for bit
+  FUSED   libbmfr's production frame path (K1 + K2, library_powr = 1) --
+          output and temporal state bit for bit
+and the reference's default build (contraction on, implementation-defined
+division) within relative L2 1e-4 on the output.  The reference's outputs
+are also checked against the SHA-256 digests in
+tests/golden/fullsize_digests.json (tests/golden/make_fullsize_digests.py)
+when that file has the configuration."""
+from __future__ import annotations
+
+import dataclasses
+import hashlib
+import json
+import os
+
+import pytest
+import torch
+
+import bmfr_amd
+import ref_run
+from ref_configs import FULL_REF_CONFIGS
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DIGESTS = os.path.join(HERE, "golden", "fullsize_digests.json")
+STAGE_KEYS = ("tmp_noisy", "tmp_fit", "weights", "mins_maxs", "filtered", "acc", "tone", "result", "spp",
+              "accept", "prev_pixel", "noisy")
+# (test id, reference build, half input planes)
+CASES = [("f1920x1080_h13", "f1920x1080_h13", 0), ("f3840x2160_h13", "f3840x2160_h13", 0),
+         ("f3840x2160_f13", "f3840x2160_f13", 0), ("f3840x2160_h16", "f3840x2160_h16", 0),
+         ("f3840x2160_h16_in16", "f3840x2160_h16", 1), ("f1280x720_h13", "f1280x720_h13", 0)]
+
+
+def bits(t: torch.Tensor) -> torch.Tensor:
+    """Raw bits of a float tensor (NaN-safe bitwise comparison)."""
+    t = t.reshape(-1)
+    if t.dtype == torch.float32:
+        return t.view(torch.int32)
+    if t.dtype == torch.float16:
+        return t.view(torch.int16)
+    return t
+
+
+def assert_same(a: torch.Tensor, b: torch.Tensor, what: str) -> None:
+    a, b = bits(a), bits(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    if not torch.equal(a, b):
+        bad = torch.nonzero(a != b).reshape(-1)
+        raise AssertionError(f"{what}: {bad.numel()} of {a.numel()} differ, first at {bad[:5].tolist()}")
+
+
+def rel_l2(a: torch.Tensor, b: torch.Tensor) -> float:
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return float(torch.linalg.norm(a - b) / torch.linalg.norm(b))
+
+
+def sha(t: torch.Tensor) -> str:
+    return hashlib.sha256(bits(t).cpu().numpy().tobytes()).hexdigest()
+
+
+def frame_planes(rc, f: int, half: int):
+    """The synthetic frame f (GPU renderer); with half, rounded to half3 --
+    what the half-input path reads -- and the reference gets those values widened."""
+    fr = bmfr_amd.synth_frame_device(rc.width, rc.height, f, seed=rc.seed)
+    if half:
+        h = {k: fr[k].half() for k in ("noisy", "normals", "positions", "albedo")}
+        return h, {k: v.float() for k, v in h.items()}
+    return fr, fr
+
+
+def cameras(rc, f: int):
+    vp, _ = bmfr_amd.synth_camera(rc.width, rc.height, max(f - 1, 0))
+    _, jit = bmfr_amd.synth_camera(rc.width, rc.height, f)
+    return vp, jit
+
+
+def hip_cfg(rc, half_in: int) -> bmfr_amd.BmfrConfig:
+    return bmfr_amd.BmfrConfig(image_width=rc.width, image_height=rc.height, not_scaled=rc.not_scaled,
+                               scaled=rc.scaled, use_half_precision_in_tmp_data=rc.half_tmp,
+                               position_limit_squared=rc.position_limit_squared,
+                               normal_limit_squared=rc.normal_limit_squared, library_powr=1, input_half=half_in)
+
+
+@pytest.mark.parametrize("case,build,half_in", CASES, ids=[c[0] for c in CASES])
+def test_fullsize_matches_reference_kernels(case, build, half_in, gpu):
+    rc = FULL_REF_CONFIGS[build]
+    for mode in ("strict", "default"):
+        if not ref_run.available(build, mode):
+            pytest.skip(f"reference build {build}_{mode} missing (oracle/build_ref.py)")
+    want = {}
+    if os.path.exists(DIGESTS):
+        with open(DIGESTS) as fh:
+            want = json.load(fh).get(case, {})
+    ref = ref_run.RefLoop(rc, "strict")
+    ref_default = ref_run.RefLoop(rc, "default")
+    stages = None if half_in else bmfr_amd.StagePipeline(hip_cfg(rc, 0))
+    den = bmfr_amd.Denoiser(hip_cfg(rc, half_in))
+    n = rc.width * rc.height
+    got_digests, worst = [], 0.0
+    for f in range(rc.frames):
+        planes, wide = frame_planes(rc, f, half_in)
+        vp, jit = cameras(rc, f)
+        rec = {}
+        ref.upload(wide["noisy"], wide["normals"], wide["positions"], wide["albedo"])
+        ref.run_stages(vp, jit, f, record=rec)
+        ref.swap()
+        dflt = {}
+        ref_default.upload(wide["noisy"], wide["normals"], wide["positions"], wide["albedo"])
+        ref_default.run_stages(vp, jit, f, record=dflt)
+        ref_default.swap()
+        if stages is not None:
+            srec = {}
+            stages.upload(wide["noisy"], wide["normals"], wide["positions"], wide["albedo"])
+            stages.run_stages(vp, jit, f, record=srec)
+            stages.swap()
+            for k in STAGE_KEYS:
+                assert_same(srec[k][:rec[k].numel()], rec[k], f"{case} frame {f} stages {k}")
+            del srec
+        den.process_frame(planes["noisy"], planes["normals"], planes["positions"], planes["albedo"], vp, jit, f)
+        fused = {
+            "result": den.copy_output(torch.empty(3 * n, device="cuda")),
+            "acc": den.copy_state("filtered_accumulated", torch.empty(3 * n, device="cuda")),
+            "noisy": den.copy_state("noisy_accumulated", torch.empty(3 * n, device="cuda")),
+            "spp": den.copy_state("spp", torch.empty(n, dtype=torch.uint8, device="cuda")),
+            "prev_pixel": den.copy_state("prev_frame_pixel", torch.empty(2 * n, device="cuda")),
+        }
+        for k, v in fused.items():
+            assert_same(v, rec[k], f"{case} frame {f} fused {k}")
+        worst = max(worst, rel_l2(fused["result"], dflt["result"]))
+        got_digests.append({"result": sha(rec["result"]), "spp": sha(rec["spp"])})
+        if want:
+            assert got_digests[-1] == want["frames"][f], f"{case} frame {f}: reference output digest changed"
+        del rec, dflt, fused
+    print(f"{case}: {rc.frames} frames bit-exact vs the reference; worst rel-L2 vs its default build {worst:.3e}")
+    assert worst <= 1e-4, worst
+
+
+def test_noise_batch_boundary_matches_reference(gpu):
+    """70 frames at 128x80: the noise table is cached kNoiseFrames = 64 frames
+    at a time, so frames 63 -> 64 cross a batch; bmfr_process_frame and
+    bmfr_process_sequence (chunks [0, 62), [62, 70)) against the reference
+    kernels on every frame."""
+    from ref_configs import REF_CONFIGS
+    rc = dataclasses.replace(REF_CONFIGS["s128x80_h13"], frames=70)  # same -D set: the same reference build
+    if not ref_run.available(rc.name, "strict"):
+        pytest.skip("reference build missing")
+    ref = ref_run.RefLoop(rc, "strict")
+    den = bmfr_amd.Denoiser(hip_cfg(rc, 0))
+    seq = bmfr_amd.Denoiser(hip_cfg(rc, 0))
+    n = rc.width * rc.height
+    frames = [frame_planes(rc, f, 0)[0] for f in range(rc.frames)]
+    cams = [cameras(rc, f) for f in range(rc.frames)]
+    outs = [torch.full((3 * n,), float("nan"), device="cuda") for _ in range(rc.frames)]
+    seq.process_sequence(frames[:62], cams[:62], 0, outputs=outs[:62])
+    seq.process_sequence(frames[62:], cams[62:], 62, outputs=outs[62:])
+    for f in range(rc.frames):
+        fr = frames[f]
+        rec = {}
+        ref.upload(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"])
+        ref.run_stages(*cams[f], f, record=rec)
+        ref.swap()
+        den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], *cams[f], f)
+        assert_same(den.copy_output(torch.empty(3 * n, device="cuda")), rec["result"], f"frame {f} per-frame")
+        torch.cuda.synchronize()
+        assert_same(outs[f], rec["result"], f"frame {f} sequence")

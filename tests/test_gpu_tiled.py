@@ -106,3 +106,52 @@ def test_tiled_matches_untiled_bitwise(shape, half, split, kernel_copy, gpu):
                 b = _tile_of(want[k], (0, 0, W, H), tile, ch)
                 bad = np.argwhere(a != b)
                 assert bad.size == 0, (shape, half, f, r, k, len(bad), bad[:3].tolist())
+
+
+def test_8k_tiled_4x2_matches_untiled(gpu):
+    """BASELINE config 4 at its own size: 7680x4320 as bench.py's 4x2 grid
+    (halo 64), every frame split into bmfr_process_frame_interior, the
+    bmfr_halo_copy exchange and bmfr_process_frame_border, == the untiled 8K
+    frame bit for bit (output and exchanged state), 3 frames."""
+    W, H, halo = 7680, 4320, 64
+    grid = TileGrid(W, H, 4, 2, halo=halo)
+    full = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    tiles = [bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H, tile=grid.tile(r),
+                                                   tile_halo=halo)) for r in range(grid.ranks)]
+    loop = LoopbackTransport(grid)
+    prev = [None] * grid.ranks
+    n = W * H
+    for f in range(3):
+        vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+        _, jit = bmfr_amd.synth_camera(W, H, f)
+        fr = bmfr_amd.synth_frame_device(W, H, f)
+        full.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, f)
+        del fr
+        inps = [bmfr_amd.synth_region_device(W, H, d.region, f) for d in tiles]
+        kws = [dict(prev_normals=p["normals"], prev_positions=p["positions"]) if p else {} for p in prev]
+        args = [(i["noisy"], i["normals"], i["positions"], i["albedo"], vp, jit, f) for i in inps]
+        if f == 0:
+            for r in range(grid.ranks):
+                tiles[r].process_frame(*args[r], **kws[r])
+        else:
+            for r in range(grid.ranks):
+                tiles[r].process_frame_interior(*args[r], **kws[r])
+            loop.exchange_all_ctx(tiles)
+            for r in range(grid.ranks):
+                tiles[r].process_frame_border(*args[r], **kws[r])
+        prev = inps
+        want = {"result": full.copy_output(torch.empty(3 * n, device="cuda")).view(H, W, 3),
+                "filtered_accumulated": full.copy_state("filtered_accumulated",
+                                                        torch.empty(3 * n, device="cuda")).view(H, W, 3),
+                "noisy_accumulated": full.copy_state("noisy_accumulated", torch.empty(3 * n, device="cuda")).view(H, W, 3)}
+        for r, d in enumerate(tiles):
+            assert d.halo_status() == 0
+            rx, ry, rw, rh = d.region
+            x, y, w, h = grid.tile(r)
+            for k, v in want.items():
+                t = torch.empty(3 * rw * rh, device="cuda")
+                got = (d.copy_output(t) if k == "result" else d.copy_state(k, t)).view(rh, rw, 3)
+                a = got[y - ry:y - ry + h, x - rx:x - rx + w].contiguous().view(torch.int32)
+                b = v[y:y + h, x:x + w].contiguous().view(torch.int32)
+                assert torch.equal(a, b), (f, r, k, int((a != b).sum()))
+        del want
