@@ -133,12 +133,23 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
             q[k] = __builtin_elementwise_fma(r, vy, q0);
         }
     } else {
-        float c2s = c2;  // opaque: keeps the products inside this (cold) branch
-        asm volatile("" : "+v"(c2s));
+        // Cold (never taken on finite data): IEEE division, one row pair per
+        // iteration of a rolled loop that rotates u and q by one pair, so the
+        // code stays small; after 8 rotations both are back in order.
+        float uu[kSlots];
 #pragma unroll
-        for (int j = 0; j < kSlots; ++j) {
-            q[j >> 1][j & 1] = (u[j] * c2s) / ulen2;
-            __builtin_amdgcn_sched_barrier(0);  // never taken in practice: keep it narrow
+        for (int j = 0; j < kSlots; ++j) uu[j] = u[j];
+#pragma unroll 1
+        for (int k = 0; k < kSlots / 2; ++k) {
+            const f2v qk = {(uu[0] * c2) / ulen2, (uu[1] * c2) / ulen2};
+            const float u0 = uu[0], u1 = uu[1];
+#pragma unroll
+            for (int j = 0; j < kSlots - 2; ++j) uu[j] = uu[j + 2];
+            uu[kSlots - 2] = u0;
+            uu[kSlots - 1] = u1;
+#pragma unroll
+            for (int i = 0; i < kSlots / 2 - 1; ++i) q[i] = q[i + 1];
+            q[kSlots / 2 - 1] = qk;
         }
     }
     q[0].x = l >= c ? q[0].x : 0.f;  // x - (+0) == x: rows above the pivot keep their value
@@ -151,13 +162,19 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
 // Step 0: column 0 is FEATURE_BUFFERS[0] = 1.f, so u = (1 - 32, 1, 1, ...),
 // |u|^2 = 1984 and u*x = x exactly (see k_fused's qr_column<0>).  Noise is
 // added to feature columns on this first load (bmfr.cl:625-627).
-template <bool NOISE>
-__device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const double* __restrict__ noise, double noise2) {
+// noise: the column's 1024 noise terms, or null (colour columns get none);
+// pre: this lane's 16 of them already loaded (the wave's first column).
+__device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const double* __restrict__ noise,
+                                               const double (&pre)[kSlots], bool use_pre) {
     float x[kSlots];
 #pragma unroll
-    for (int j = 0; j < kSlots; ++j) {
-        x[j] = hget(a, j);
-        if (NOISE) {
+    for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
+    if (use_pre) {  // wave-uniform
+#pragma unroll
+        for (int j = 0; j < kSlots; ++j) x[j] = (float)((double)x[j] + pre[j]);
+    } else if (noise) {  // wave-uniform
+#pragma unroll
+        for (int j = 0; j < kSlots; ++j) {
             x[j] = (float)((double)x[j] + noise[l + 64 * j]);
             if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // 8 double loads in flight at a time
         }
@@ -242,36 +259,40 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B>& L, int l
 // wait for its global loads and stores (__syncthreads() does).
 __device__ __forceinline__ void k1_barrier() { lds_barrier(); }
 
-// Wave W's part of the fit: columns c = W (mod 4), c >= 1 (column 0 is implicit).
-template <int W, int NS, int FS>
+// Wave W's part of the fit: columns c = W + 4 k (slot k), c >= 1 (column 0
+// is implicit).  W is a run-time (wave-uniform) value, so the four waves run
+// one copy of the code: column ownership is a scalar branch, while the slot
+// of every column a step touches is known at compile time.
+template <int NS, int FS>
 struct WaveFit {
     static constexpr int B = NS + FS + 3;
     static constexpr int NF = B - 3;  // pivot columns
     static constexpr int NSL = (B + 3) / 4;
-    static constexpr bool owns(int c) { return c >= 1 && c < B && (c & 3) == W; }
+    static __device__ __forceinline__ bool owns(int W, int c) { return c >= 1 && c < B && (c & 3) == W; }
+
+    // The first column a wave updates at step 0 (slot 0, or slot 1 for wave
+    // 0, whose slot 0 is column 0): a feature column for every wave.
+    static __device__ __forceinline__ int first_column(int W) { return W == 0 ? 4 : W; }
 
     template <int c>
-    static __device__ __forceinline__ void step(h2 (&a)[NSL][8], Lds<B>& L, int l, const double* __restrict__ noise,
-                                                double noise2) {
-        constexpr int nxt = c + 1;
-        constexpr bool publish = nxt < NF && owns(nxt);
+    static __device__ __forceinline__ void step(h2 (&a)[NSL][8], Lds<B>& L, int W, int l,
+                                                const double* __restrict__ noise, const double (&pre)[kSlots]) {
+        constexpr int nxt = c + 1;  // the next pivot column, slot nxt >> 2 of wave nxt & 3
+        const bool publish = nxt < NF && W == (nxt & 3);
         if constexpr (c == 0) {
-            if constexpr (publish) {
-                update_column0<(nxt < NF)>(a[nxt >> 2], l, noise + (nxt - 1) * kBlockPixels, noise2);
+            if (publish) {  // column 1 of wave 1: its first column
+                update_column0(a[nxt >> 2], l, noise + (nxt - 1) * kBlockPixels, pre, true);
                 publish_pivot<nxt, B>(a[nxt >> 2], L, l);
             }
             sfor<NSL>([&](auto K) {
-                constexpr int fb = W + 4 * decltype(K)::value;
-                if constexpr (owns(fb) && !(publish && fb == nxt))
-                    update_column0<(fb < NF)>(a[fb >> 2], l, noise + (fb - 1) * kBlockPixels, noise2);
+                constexpr int k = decltype(K)::value;
+                const int fb = W + 4 * k;
+                if (owns(W, fb) && !(publish && fb == nxt))
+                    update_column0(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr, pre,
+                                   fb == first_column(W));
             });
         } else {
-            constexpr bool any = [] {
-                for (int fb = c + 1; fb < B; ++fb)
-                    if (owns(fb)) return true;
-                return false;
-            }();
-            if constexpr (any) {
+            if (W + 4 * (NSL - 1) > c) {  // some column of this wave is past the pivot
                 float u[kSlots];
                 const float4* src = reinterpret_cast<const float4*>(&L.u[c & 1][l * kUStride]);
 #pragma unroll
@@ -283,15 +304,17 @@ struct WaveFit {
                     u[4 * q + 3] = v.w;
                 }
                 const float ulen2 = L.piv[c & 1][0], recip = L.piv[c & 1][1];
-                if constexpr (publish) {
-                    // the next pivot is every wave's critical path: issue it first
-                    update_column<c>(a[nxt >> 2], u, ulen2, recip, l);
-                    publish_pivot<nxt, B>(a[nxt >> 2], L, l);
+                if constexpr (nxt < NF) {
+                    if (publish) {  // the next pivot is every wave's critical path: issue it first
+                        update_column<c>(a[nxt >> 2], u, ulen2, recip, l);
+                        publish_pivot<nxt, B>(a[nxt >> 2], L, l);
+                    }
                 }
                 sfor<NSL>([&](auto K) {
-                    constexpr int fb = W + 4 * decltype(K)::value;
-                    if constexpr (owns(fb) && fb > c && !(publish && fb == nxt))
-                        update_column<c>(a[fb >> 2], u, ulen2, recip, l);
+                    constexpr int k = decltype(K)::value;
+                    const int fb = W + 4 * k;
+                    if (4 * k + 3 > c && owns(W, fb) && fb > c && !(publish && fb == nxt))
+                        update_column<c>(a[k], u, ulen2, recip, l);
                 });
             }
         }
@@ -299,33 +322,42 @@ struct WaveFit {
     }
 
     template <int... C>
-    static __device__ __forceinline__ void steps(h2 (&a)[NSL][8], Lds<B>& L, int l, const double* __restrict__ noise,
-                                                 double noise2, std::integer_sequence<int, C...>) {
-        (step<C>(a, L, l, noise, noise2), ...);
+    static __device__ __forceinline__ void steps(h2 (&a)[NSL][8], Lds<B>& L, int W, int l,
+                                                 const double* __restrict__ noise, const double (&pre)[kSlots],
+                                                 std::integer_sequence<int, C...>) {
+        (step<C>(a, L, W, l, noise, pre), ...);
     }
 
-    // after_load(): runs once the matrix is in registers and the LDS area is free.
-    template <class AfterLoad>
-    static __device__ __forceinline__ void run(Lds<B>& L, int l, const double* __restrict__ noise, double noise2,
-                                               AfterLoad&& after_load) {
+    // Step 0's noise for the wave's first column, loaded while the last
+    // items of phase 1 finish (it is every wave's first dependent load of the fit).
+    static __device__ __forceinline__ void prefetch_noise(int W, int l, const double* __restrict__ noise,
+                                                          double (&pre)[kSlots]) {
+        const double* src = noise + (first_column(W) - 1) * kBlockPixels + l;
+#pragma unroll
+        for (int j = 0; j < kSlots; ++j) pre[j] = src[64 * j];
+    }
+
+    static __device__ __forceinline__ void run(Lds<B>& L, int W, int l, const double* __restrict__ noise,
+                                               const double (&pre)[kSlots]) {
         h2 a[NSL][8];
         sfor<NSL>([&](auto K) {
-            constexpr int c = W + 4 * decltype(K)::value;
-            if constexpr (owns(c)) {
+            constexpr int k = decltype(K)::value;
+            const int c = W + 4 * k;
+            if (owns(W, c)) {
                 // pair p of lane l's row slot sits at dword p ^ ((l >> 2) & 7) (see phase 1)
                 const uint32_t* src = reinterpret_cast<const uint32_t*>(&L.M[c - 1][l * kSlots]);
                 const int q = (l >> 2) & 7;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) a[c >> 2][i] = __builtin_bit_cast(h2, src[i ^ q]);
+                for (int i = 0; i < 8; ++i) a[k][i] = __builtin_bit_cast(h2, src[i ^ q]);
             }
         });
         k1_barrier();  // the u buffers alias M
-        after_load();
 
         // Scale the position features to the block's [min, max] (bmfr.cl:510-542).
         sfor<NSL>([&](auto K) {
-            constexpr int c = W + 4 * decltype(K)::value;
-            if constexpr (owns(c) && c >= NS && c < NF) {
+            constexpr int k = decltype(K)::value;
+            const int c = W + 4 * k;
+            if (owns(W, c) && c >= NS && c < NF) {
                 float hi[4], lo[4];
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
@@ -333,7 +365,7 @@ struct WaveFit {
                     lo[m] = INFINITY;
 #pragma unroll
                     for (int si = 0; si < 4; ++si) {
-                        const float v = hget(a[c >> 2], m + 4 * si);
+                        const float v = hget(a[k], m + 4 * si);
                         hi[m] = fmaxf(v, hi[m]);
                         lo[m] = fminf(v, lo[m]);
                     }
@@ -350,20 +382,21 @@ struct WaveFit {
                 }
 #pragma unroll
                 for (int j = 0; j < kSlots; ++j) {
-                    const float v = hget(a[c >> 2], j) - bmin;
-                    a[c >> 2][j >> 1][j & 1] = (_Float16)(divide ? div_by_recip(v, d, rcp) : v);
+                    const float v = hget(a[k], j) - bmin;
+                    a[k][j >> 1][j & 1] = (_Float16)(divide ? div_by_recip(v, d, rcp) : v);
                 }
             }
         });
         if (W == 0 && l < 3) L.R[l] = 32.f;  // R(0,0) = |column 0|
 
-        steps(a, L, l, noise, noise2, std::make_integer_sequence<int, NF>{});
+        steps(a, L, W, l, noise, pre, std::make_integer_sequence<int, NF>{});
 
         // Right-hand side: rows 0..B-4 of the colour columns (bmfr.cl:596-600).
         sfor<NSL>([&](auto K) {
-            constexpr int c = W + 4 * decltype(K)::value;
-            if constexpr (owns(c) && c >= NF) {
-                if (l < NF) L.R[((B - 3) * (B - 2) + l) * 3 + (c - NF)] = hget(a[c >> 2], 0);
+            constexpr int k = decltype(K)::value;
+            const int c = W + 4 * k;
+            if (owns(W, c) && c >= NF) {
+                if (l < NF) L.R[((B - 3) * (B - 2) + l) * 3 + (c - NF)] = hget(a[k], 0);
             }
         });
     }
@@ -415,6 +448,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 #define BMFR_STAMP(k) (void)0
 #endif
     BMFR_STAMP(0);
+#ifdef BMFR_P1_PRIO
+    __builtin_amdgcn_s_setprio(BMFR_P1_PRIO);
+#endif
     int bx, by;
     k1_block(P, g, bx, by);
     const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
@@ -466,18 +502,17 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
         }
     }
     report_reach(P, A.reach, over);
+#ifdef BMFR_P1_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+    double pre[kSlots];
+    WaveFit<NS, FS>::prefetch_noise(w, l, A.noise, pre);
     k1_barrier();  // matrix in LDS; phase 1's global stores drain in the background
     BMFR_STAMP(1);
     BMFR_STAMP(2);  // scaling runs inside the per-wave fit
 
     // ---- fit: min/max scaling, Householder QR, right-hand side ----
-    const auto park = [] {};
-    switch (w) {
-        case 0: WaveFit<0, NS, FS>::run(L, l, A.noise, P.noise2, park); break;
-        case 1: WaveFit<1, NS, FS>::run(L, l, A.noise, P.noise2, park); break;
-        case 2: WaveFit<2, NS, FS>::run(L, l, A.noise, P.noise2, park); break;
-        default: WaveFit<3, NS, FS>::run(L, l, A.noise, P.noise2, park); break;
-    }
+    WaveFit<NS, FS>::run(L, w, l, A.noise, pre);
     // Phase 3's loads (normal and position of the four items, bmfr.cl:725-729)
     // go out now: they land while wave 0 back-substitutes and the others wait.
     int l3 = l;  // opaque copy: recompute phase-1 addresses instead of keeping them live across the fit
@@ -563,6 +598,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 // memory-bound phase 1 and VALU-bound fit in lockstep (large launches only,
 // not a tile's border ring).
 __device__ __forceinline__ void k1_stagger(int b, int n) {
+#ifdef BMFR_NO_STAGGER
+    return;
+#endif
     if (b < 4 * 256 && n >= 8 * 256) {
         const int k = ((b >> 8) & 3) * (kStagger / 8000);
         for (int s = 0; s < k; ++s) __builtin_amdgcn_s_sleep(125);

@@ -102,7 +102,7 @@ bool parse_header(const std::vector<uint8_t>& file, ExrHeader& h, size_t& end, s
         if (name.empty()) break;
         const std::string type = r.cstr();
         const int32_t size = r.get<int32_t>();
-        if (!r.ok || size < 0 || r.p + (size_t)size > file.size()) return err = "truncated attribute " + name, false;
+        if (!r.ok || size < 0 || (size_t)size > file.size() - r.p) return err = "truncated attribute " + name, false;
         const size_t next = r.p + size;
         if (name == "channels" && type == "chlist") {
             while (r.p < next) {
@@ -116,6 +116,7 @@ bool parse_header(const std::vector<uint8_t>& file, ExrHeader& h, size_t& end, s
                 h.channels.push_back(c);
             }
         } else if (name == "compression") {
+            if (size < 1) return err = "bad compression attribute", false;
             h.compression = file[r.p];
         } else if (name == "dataWindow" && size == 16) {
             h.x0 = r.get<int32_t>();
@@ -123,6 +124,7 @@ bool parse_header(const std::vector<uint8_t>& file, ExrHeader& h, size_t& end, s
             h.x1 = r.get<int32_t>();
             h.y1 = r.get<int32_t>();
         } else if (name == "lineOrder") {
+            if (size < 1) return err = "bad lineOrder attribute", false;
             h.line_order = file[r.p];
         }
         r.p = next;
@@ -130,7 +132,11 @@ bool parse_header(const std::vector<uint8_t>& file, ExrHeader& h, size_t& end, s
     end = r.p;
     if (h.tiled) return err = "tiled OpenEXR files are not supported", false;
     if (lines_per_chunk(h.compression) == 0) return err = "unsupported OpenEXR compression " + std::to_string(h.compression), false;
-    if (h.channels.empty() || h.width() <= 0 || h.height() <= 0) return err = "bad channels / data window", false;
+    // data window extents in 64-bit (x1 - x0 overflows int for hostile corners)
+    const int64_t w64 = (int64_t)h.x1 - h.x0 + 1, h64 = (int64_t)h.y1 - h.y0 + 1;
+    if (h.channels.empty() || w64 <= 0 || h64 <= 0 || w64 > (1 << 20) || h64 > (1 << 20) ||
+        h.channels.size() > 1024)
+        return err = "bad channels / data window", false;
     for (const Channel& c : h.channels)
         if (c.xs != 1 || c.ys != 1 || c.type < 0 || c.type > 2) return err = "subsampled or unknown channel " + c.name, false;
     return true;
@@ -303,17 +309,18 @@ int bmfr_exr_read_rgb(const char* path, int width, int height, float* rgb) {
     }
     const int lpc = lines_per_chunk(h.compression);
     const int chunks = (height + lpc - 1) / lpc;
-    if (p + (size_t)chunks * 8 > file.size()) return fail(std::string(path) + ": truncated offset table");
+    if (p > file.size() || (size_t)chunks > (file.size() - p) / 8) return fail(std::string(path) + ": truncated offset table");
     std::vector<uint8_t> raw;
     for (int c = 0; c < chunks; ++c) {
         uint64_t off;
         std::memcpy(&off, file.data() + p + 8 * (size_t)c, 8);
-        if (off + 8 > file.size()) return fail(std::string(path) + ": bad chunk offset");
+        // (compared without overflow: an offset near 2^64 must not wrap)
+        if (file.size() < 8 || off > file.size() - 8) return fail(std::string(path) + ": bad chunk offset");
         int32_t y, size;
         std::memcpy(&y, file.data() + off, 4);
         std::memcpy(&size, file.data() + off + 4, 4);
         const int line0 = y - h.y0;
-        if (line0 < 0 || line0 >= height || size < 0 || off + 8 + (uint64_t)size > file.size())
+        if (line0 < 0 || line0 >= height || size < 0 || (uint64_t)size > file.size() - off - 8)
             return fail(std::string(path) + ": bad chunk");
         const int lines = std::min(lpc, height - line0);
         if (!decode_chunk(h.compression, file.data() + off + 8, (size_t)size, line_bytes * lines, raw))

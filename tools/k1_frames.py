@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""K1 / K2 device time of every frame of the synthetic sequence (libbmfr's
+profiling events, stride 1), to see how the per-frame cost moves along the
+sequence (spp growth, reprojection acceptance).
+
+  python tools/k1_frames.py [W H FRAMES]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bmfr_amd  # noqa: E402
+
+W, H, N = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (3840, 2160, 100)))
+den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+frames = [bmfr_amd.synth_frame_device(W, H, f) for f in range(N)]
+den.set_profiling(True, capacity=N, stride=1)
+for f in range(N):
+    vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+    _, jit = bmfr_amd.synth_camera(W, H, f)
+    fr = frames[f]
+    den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, f)
+torch.cuda.synchronize()
+prof = den.profile()
+k1 = np.array([p[1] for p in prof])
+k2 = np.array([p[2] for p in prof])
+for lo in range(0, N, 10):
+    print(f"frames {lo:3d}-{min(lo + 9, N - 1):3d}: K1 {k1[lo:lo + 10].mean():.4f} ms  K2 {k2[lo:lo + 10].mean():.4f} ms")
+print(f"frames 5-24 K1 {k1[5:25].mean():.4f}  frames 5-104 K1 {k1[5:].mean():.4f}")
