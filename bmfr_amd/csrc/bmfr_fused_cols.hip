@@ -9,17 +9,18 @@
 //
 //   * phase 1: thread (wave w, lane l) computes the features of rows
 //     r = l + 64 j, j = 4w..4w+3, and writes them to an LDS matrix;
-//   * fit: wave w takes COLUMNS c = w, w+4, w+8, ... -- all 1024 rows of each,
-//     lane l holding rows l + 64 j, j = 0..15 (8 packed-half registers per
-//     column).  Upstream's fitter work-item t = l + 64 m owns rows t + 256 s,
+//   * fit: wave w takes COLUMNS c = 1 + w, 5 + w, 9 + w, ... -- all 1024 rows
+//     of each, lane l holding rows l + 64 j, j = 0..15 (8 packed-half
+//     registers per column); one copy of the code serves the four waves.  Upstream's fitter work-item t = l + 64 m owns rows t + 256 s,
 //     i.e. j = m + 4 s, so each work-item partial and the first tree step
 //     (bmfr.cl:32-33) are in one lane and the rest of the tree runs on DPP /
 //     permlane swaps (bmfr_wave.h): every dot product, norm, min and max of
 //     the fit is a wave-local exact reduction, no LDS round trip, no barrier.
 //   * Householder step c needs only u_c, which the owner of column c publishes
-//     in LDS (double-buffered) as soon as it has applied step c-1 to that
-//     column, ahead of its other columns: one barrier per column instead of a
-//     block reduction per dot product.
+//     in LDS (three buffers) as soon as it has applied step c-1 to that
+//     column, ahead of its other columns, and announces with an LDS flag: a
+//     wave waits only for the pivot it needs -- no block reduction per dot
+//     product and no work-group barrier per column.
 //   * phase 3 (weighted sum + blend) per pixel again, rows of phase 1.
 //
 // The R matrix, back substitution and phase-3 code are k_fused's.  Parity:
@@ -38,19 +39,25 @@ constexpr int kSlots = 16;    // rows per lane per column (row = lane + 64 j)
 constexpr int kStagger = 24000;  // cycles between first-round work-group groups (k1_stagger)
 constexpr int kUStride = 20;     // floats per lane in a u buffer: 16 + 4 (conflict-free 16-byte reads)
 
+// Householder vectors in flight: the fit's waves wait for each published
+// pivot through an LDS flag instead of a barrier per column, so a buffer is
+// reused only once every wave has finished the step that read it.
+constexpr int kUBufs = 3;
 template <int B>
 struct Lds {
     union {
         _Float16 M[B - 1][64 * kSlots];  // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
-        float u[2][64 * kUStride];       // Householder vectors, double-buffered by column parity
+        float u[kUBufs][64 * kUStride];  // Householder vectors, u_c in buffer c % kUBufs
     };
     float keep[4][3][kThreads];  // phase 1 -> 3: previous accumulated filtered colour per item
-    float piv[2][2];                    // |u|^2 and RN(1/|u|^2) of the published vector
+    float piv[kUBufs][2];               // |u|^2 and RN(1/|u|^2) of the published vector
+    int pub;                            // highest published pivot column
+    int prog[4];                        // per wave: the last step it has applied
     float R[(B - 2) * (B - 2) * 3];     // R[x][y][ch], x = column (as k_fused)
     float weights[(B - 3) * 3];
     float mm[3 * (B - 3)];              // per scaled feature: min, max, 1/(max-min)
 };
-static_assert(sizeof(float) * 2 * 64 * kUStride <= sizeof(_Float16) * 12 * 64 * kSlots,
+static_assert(sizeof(float) * kUBufs * 64 * kUStride <= sizeof(_Float16) * 12 * 64 * kSlots,
               "u buffers must fit in the matrix area (B >= 13)");
 
 template <int... I, class F>
@@ -210,6 +217,23 @@ __device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const double* 
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// LDS flags of the fit: wave-uniform polls with a short sleep.  A publisher
+// waits for lgkmcnt(0) before raising the flag, so the data it wrote is in
+// LDS before any wave can see the flag.
+// The polls are bounded (~2^20 sleeps): a scheduling bug would then give
+// wrong results instead of a wave that never finishes.
+constexpr int kMaxPolls = 1 << 20;
+__device__ __forceinline__ void wait_pub(const int* pub, int c) {
+    for (int k = 0; k < kMaxPolls && __hip_atomic_load(pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c; ++k)
+        __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void wait_all_progress(const int* prog, int c) {
+    for (int w = 0; w < 4; ++w)
+        for (int k = 0;
+             k < kMaxPolls && __hip_atomic_load(&prog[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c; ++k)
+            __builtin_amdgcn_s_sleep(1);
+}
+
 // The owner of pivot column c (>= 1), once steps 0..c-1 are applied to it:
 // |x|^2 over rows >= c+1, the Householder vector u and |u|^2 (bmfr.cl:555-601),
 // published to LDS with the R column.
@@ -238,12 +262,14 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B>& L, int l
     const float ucl2 = ucl - vlen;
     const float ulen2 = sumsq + ucl2 * ucl2;
     if (l == c) x[0] = ucl2;
-    float4* dst = reinterpret_cast<float4*>(&L.u[c & 1][l * kUStride]);
+    constexpr int buf = c % kUBufs;
+    if constexpr (c >= kUBufs) wait_all_progress(L.prog, c - kUBufs);  // readers of u_{c-3} done
+    float4* dst = reinterpret_cast<float4*>(&L.u[buf][l * kUStride]);
 #pragma unroll
     for (int q = 0; q < 4; ++q) dst[q] = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
     if (l == 0) {
-        L.piv[c & 1][0] = ulen2;
-        L.piv[c & 1][1] = 1.f / ulen2;
+        L.piv[buf][0] = ulen2;
+        L.piv[buf][1] = 1.f / ulen2;
     }
     if (l < c) {  // R column: rows above the diagonal, then the diagonal
 #pragma unroll
@@ -253,48 +279,53 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B>& L, int l
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) L.R[(c * RE + c) * 3 + ch] = vlen;
     }
+    // u_c and |u_c|^2 in LDS before the flag says so
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    if (l == 0) __hip_atomic_store(&L.pub, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // The work-group shares data through LDS only, so its barriers need not
 // wait for its global loads and stores (__syncthreads() does).
 __device__ __forceinline__ void k1_barrier() { lds_barrier(); }
 
-// Wave W's part of the fit: columns c = W + 4 k (slot k), c >= 1 (column 0
-// is implicit).  W is a run-time (wave-uniform) value, so the four waves run
-// one copy of the code: column ownership is a scalar branch, while the slot
-// of every column a step touches is known at compile time.
+// Wave W's part of the fit: columns c = 1 + W + 4 k (slot k); column 0 is
+// implicit.  W is a run-time (wave-uniform) value, so the four waves run one
+// copy of the code: column ownership is a scalar branch, while the slot of
+// every column a step touches is known at compile time.
 template <int NS, int FS>
 struct WaveFit {
     static constexpr int B = NS + FS + 3;
     static constexpr int NF = B - 3;  // pivot columns
-    static constexpr int NSL = (B + 3) / 4;
-    static __device__ __forceinline__ bool owns(int W, int c) { return c >= 1 && c < B && (c & 3) == W; }
+    static constexpr int NSL = (B + 2) / 4;
+    static __device__ __forceinline__ bool owns(int W, int c) { return c >= 1 && c < B && ((c - 1) & 3) == W; }
+    static constexpr int owner(int c) { return (c - 1) & 3; }
+    static constexpr int slot(int c) { return (c - 1) >> 2; }
 
-    // The first column a wave updates at step 0 (slot 0, or slot 1 for wave
-    // 0, whose slot 0 is column 0): a feature column for every wave.
-    static __device__ __forceinline__ int first_column(int W) { return W == 0 ? 4 : W; }
+    // The first column a wave updates at step 0: a feature column for every wave.
+    static __device__ __forceinline__ int first_column(int W) { return 1 + W; }
 
     template <int c>
     static __device__ __forceinline__ void step(h2 (&a)[NSL][8], Lds<B>& L, int W, int l,
                                                 const double* __restrict__ noise, const double (&pre)[kSlots]) {
-        constexpr int nxt = c + 1;  // the next pivot column, slot nxt >> 2 of wave nxt & 3
-        const bool publish = nxt < NF && W == (nxt & 3);
+        constexpr int nxt = c + 1;  // the next pivot column, slot(nxt) of wave owner(nxt)
+        const bool publish = nxt < NF && W == owner(nxt);
         if constexpr (c == 0) {
-            if (publish) {  // column 1 of wave 1: its first column
-                update_column0(a[nxt >> 2], l, noise + (nxt - 1) * kBlockPixels, pre, true);
-                publish_pivot<nxt, B>(a[nxt >> 2], L, l);
+            if (publish) {  // column 1 of wave 0: its first column
+                update_column0(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre, true);
+                publish_pivot<nxt, B>(a[slot(nxt)], L, l);
             }
             sfor<NSL>([&](auto K) {
                 constexpr int k = decltype(K)::value;
-                const int fb = W + 4 * k;
+                const int fb = 1 + W + 4 * k;
                 if (owns(W, fb) && !(publish && fb == nxt))
                     update_column0(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr, pre,
                                    fb == first_column(W));
             });
         } else {
-            if (W + 4 * (NSL - 1) > c) {  // some column of this wave is past the pivot
+            if (1 + W + 4 * ((B - 2 - W) / 4) > c) {  // this wave's last column is past the pivot
+                wait_pub(&L.pub, c);
                 float u[kSlots];
-                const float4* src = reinterpret_cast<const float4*>(&L.u[c & 1][l * kUStride]);
+                const float4* src = reinterpret_cast<const float4*>(&L.u[c % kUBufs][l * kUStride]);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const float4 v = src[q];
@@ -303,22 +334,25 @@ struct WaveFit {
                     u[4 * q + 2] = v.z;
                     u[4 * q + 3] = v.w;
                 }
-                const float ulen2 = L.piv[c & 1][0], recip = L.piv[c & 1][1];
+                const float ulen2 = L.piv[c % kUBufs][0], recip = L.piv[c % kUBufs][1];
                 if constexpr (nxt < NF) {
                     if (publish) {  // the next pivot is every wave's critical path: issue it first
-                        update_column<c>(a[nxt >> 2], u, ulen2, recip, l);
-                        publish_pivot<nxt, B>(a[nxt >> 2], L, l);
+                        update_column<c>(a[slot(nxt)], u, ulen2, recip, l);
+                        publish_pivot<nxt, B>(a[slot(nxt)], L, l);
                     }
                 }
                 sfor<NSL>([&](auto K) {
                     constexpr int k = decltype(K)::value;
-                    const int fb = W + 4 * k;
-                    if (4 * k + 3 > c && owns(W, fb) && fb > c && !(publish && fb == nxt))
-                        update_column<c>(a[k], u, ulen2, recip, l);
+                    const int fb = 1 + W + 4 * k;
+                    if constexpr (4 * k + 4 > c) {  // slot k holds columns <= 4k + 4
+                        if (owns(W, fb) && fb > c && !(publish && fb == nxt))
+                            update_column<c>(a[k], u, ulen2, recip, l);
+                    }
                 });
             }
         }
-        if constexpr (c + 1 < NF) k1_barrier();  // u_{c+1} published
+        // this wave is done with u_c (no barrier: a wave waits only for the pivot it needs)
+        if (l == 0) __hip_atomic_store(&L.prog[W], c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 
     template <int... C>
@@ -342,7 +376,7 @@ struct WaveFit {
         h2 a[NSL][8];
         sfor<NSL>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            const int c = W + 4 * k;
+            const int c = 1 + W + 4 * k;
             if (owns(W, c)) {
                 // pair p of lane l's row slot sits at dword p ^ ((l >> 2) & 7) (see phase 1)
                 const uint32_t* src = reinterpret_cast<const uint32_t*>(&L.M[c - 1][l * kSlots]);
@@ -351,12 +385,16 @@ struct WaveFit {
                 for (int i = 0; i < 8; ++i) a[k][i] = __builtin_bit_cast(h2, src[i ^ q]);
             }
         });
+        if (W == 0 && l < 5) {  // read only after the barrier below
+            if (l == 0) L.pub = 0;
+            else L.prog[l - 1] = -1;
+        }
         k1_barrier();  // the u buffers alias M
 
         // Scale the position features to the block's [min, max] (bmfr.cl:510-542).
         sfor<NSL>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            const int c = W + 4 * k;
+            const int c = 1 + W + 4 * k;
             if (owns(W, c) && c >= NS && c < NF) {
                 float hi[4], lo[4];
 #pragma unroll
@@ -394,7 +432,7 @@ struct WaveFit {
         // Right-hand side: rows 0..B-4 of the colour columns (bmfr.cl:596-600).
         sfor<NSL>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            const int c = W + 4 * k;
+            const int c = 1 + W + 4 * k;
             if (owns(W, c) && c >= NF) {
                 if (l < NF) L.R[((B - 3) * (B - 2) + l) * 3 + (c - NF)] = hget(a[k], 0);
             }
@@ -448,9 +486,6 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 #define BMFR_STAMP(k) (void)0
 #endif
     BMFR_STAMP(0);
-#ifdef BMFR_P1_PRIO
-    __builtin_amdgcn_s_setprio(BMFR_P1_PRIO);
-#endif
     int bx, by;
     k1_block(P, g, bx, by);
     const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
@@ -502,9 +537,6 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
         }
     }
     report_reach(P, A.reach, over);
-#ifdef BMFR_P1_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
     double pre[kSlots];
     WaveFit<NS, FS>::prefetch_noise(w, l, A.noise, pre);
     k1_barrier();  // matrix in LDS; phase 1's global stores drain in the background
@@ -598,9 +630,6 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 // memory-bound phase 1 and VALU-bound fit in lockstep (large launches only,
 // not a tile's border ring).
 __device__ __forceinline__ void k1_stagger(int b, int n) {
-#ifdef BMFR_NO_STAGGER
-    return;
-#endif
     if (b < 4 * 256 && n >= 8 * 256) {
         const int k = ((b >> 8) & 3) * (kStagger / 8000);
         for (int s = 0; s < k; ++s) __builtin_amdgcn_s_sleep(125);
