@@ -440,36 +440,46 @@ struct WaveFit {
     }
 };
 
-// Back substitution (bmfr.cl:658-699), as k_fused.
+// Back substitution (bmfr.cl:658-699) in registers: lane (ch, x) of wave 0,
+// lane = 3 x + ch, holds column x of R for colour channel ch; the values a
+// step needs from other lanes come by readlane (3 per value, one per channel,
+// selected per lane), so there is no LDS round trip between the steps.  Every
+// element sees upstream's operations in upstream's order: row i divided by
+// the diagonal, the right-hand side reduced by the already-divided row
+// entries left to right, column i scaled by x_i.
 template <int B>
-__device__ __forceinline__ void back_substitute(Lds<B>& L, int t) {
+__device__ __forceinline__ void back_substitute_regs(Lds<B>& L, int t) {
     constexpr int RE = B - 2;
     if (t >= 64) return;
     const int ch = t % 3, x = t / 3;
-    float* R = L.R;
+    float col[RE - 1];  // rows 0..RE-2 of column x
+#pragma unroll
+    for (int y = 0; y < RE - 1; ++y) col[y] = x < RE ? L.R[(x * RE + y) * 3 + ch] : 0.f;
+    // value v of lane 3 X + ch, for this lane's channel
+    auto from = [&](float v, int X) {
+        const float a = lane_value(v, 3 * X), b = lane_value(v, 3 * X + 1), c = lane_value(v, 3 * X + 2);
+        return ch == 0 ? a : (ch == 1 ? b : c);
+    };
+#pragma unroll
     for (int i = RE - 2; i >= 0; --i) {
-        const float div = R[(i * RE + i) * 3 + ch];
-        __builtin_amdgcn_wave_barrier();
-        if (x < RE && x >= i) R[(x * RE + i) * 3 + ch] = R[(x * RE + i) * 3 + ch] / div;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (x == 0) {
-            float rhs = R[((RE - 1) * RE + i) * 3 + ch];
-            for (int j = i + 1; j < RE - 1; ++j) rhs = rhs - R[(j * RE + i) * 3 + ch];
-            R[((RE - 1) * RE + i) * 3 + ch] = rhs;
+        const float div = from(col[i], i);
+        if (x < RE && x >= i) col[i] = col[i] / div;
+        float rhs = from(col[i], RE - 1);
+#pragma unroll
+        for (int j = i + 1; j < RE - 1; ++j) rhs = rhs - from(col[i], j);
+        if (x == RE - 1) col[i] = rhs;
+        if (x == i) {  // rhs is x_i on every lane of the channel
+#pragma unroll
+            for (int y = 0; y <= i; ++y) col[y] = col[y] * rhs;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        const float xi = R[((RE - 1) * RE + i) * 3 + ch];
-        if (x <= i && x < RE) R[(i * RE + x) * 3 + ch] = R[(i * RE + x) * 3 + ch] * xi;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
     }
-    if (x < B - 3) L.weights[x * 3 + ch] = R[((RE - 1) * RE + x) * 3 + ch];
+    if (x == RE - 1) {
+#pragma unroll
+        for (int y = 0; y < B - 3; ++y) L.weights[y * 3 + ch] = col[y];
+    }
 }
 
 constexpr int kColsWaves = 4;  // minimum waves per SIMD for the register allocator (128 VGPRs: 4 WGs/CU)
-constexpr int kBatch = 2;      // phase-1 items whose current-frame loads are issued together (4: > 128 VGPRs)
 
 // One K1 work-group (block g of the launch), on the LDS area L.
 template <int NS, int FS, class IN>
@@ -497,16 +507,18 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     int over = 0;        // reprojection taps outside the valid state rectangle (tiled contexts)
     // The temporal part of accumulate_filtered_data is read at the noisy
     // accumulation's taps (bmfr.cl:786-842) and parked in LDS for phase 3.
+    // Software-pipelined one item deep: item i + 1's current-frame loads go
+    // out right behind item i's reprojection taps, so each wait for taps
+    // leaves the next item's loads in flight.
+    NoisyCur cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly, frame);
 #pragma unroll
-    for (int i0 = 0; i0 < 4; i0 += kBatch) {
-        NoisyCur cur[kBatch];
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k)
-            cur[k] = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly + 2 * (i0 + k), frame);
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) {
-            const int i = i0 + k;
-            const NoisyItem it = noisy_item_spec<true, IN>(P, A.in, A.cam, cur[k], frame, A.acc_prev);
+    for (int i = 0; i < 4; ++i) {
+        const NoisyTaps tp = noisy_taps_issue<true, IN>(P, A.in, A.cam, cur, frame, A.acc_prev);
+        NoisyCur nxt;
+        if (i < 3) nxt = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly + 2 * (i + 1), frame);
+        __builtin_amdgcn_sched_barrier(0);
+        const NoisyItem it = noisy_taps_finish<true>(P, cur, tp, frame);
+        {
 #pragma unroll
             for (int f = 1; f < B; ++f) {
                 float v;
@@ -535,6 +547,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                     *reinterpret_cast<uint32_t*>(&L.M[f - 1][l * kSlots + 2 * pair]) = __builtin_bit_cast(uint32_t, pk[f]);
             }
         }
+        if (i < 3) cur = nxt;
     }
     report_reach(P, A.reach, over);
     double pre[kSlots];
@@ -562,7 +575,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     }
     k1_barrier();  // R complete (LDS); with LDS-only barriers the loads above stay in flight
     BMFR_STAMP(3);
-    back_substitute<B>(L, t);
+    back_substitute_regs<B>(L, t);
     k1_barrier();  // weights complete
     BMFR_STAMP(4);
 

@@ -269,27 +269,29 @@ __device__ __forceinline__ NoisyCur noisy_load_current(const Params& P, const No
     return c;
 }
 
+// noisy_item_spec in two halves, so a caller can issue the next item's
+// current-frame loads while this item's taps are in flight: _issue does the
+// reprojection (bmfr.cl:343-372) and issues the tap loads, _finish tests,
+// weighs and blends them (bmfr.cl:374-445).
+struct NoisyTaps {
+    f3 pp[4], pn[4], pc[4], pa[4];
+    float sp[4], wts[4];
+    uint32_t inb;  // bit i: tap i inside the image
+    float pfx, pfy, flx, fly;
+    int over;
+};
+
 template <bool FILT = false, class IN = float>
-__device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const NoisyInputs& in, const Camera& cam,
+__device__ __forceinline__ NoisyTaps noisy_taps_issue(const Params& P, const NoisyInputs& in, const Camera& cam,
                                                      const NoisyCur& c, int frame,
                                                      const float* __restrict__ acc_prev = nullptr) {
-    NoisyItem o;
-    o.owner = c.owner;
-    o.lin = pix(P, c.px, c.py);
-    o.n = c.nrm;
-    o.p = c.wp;
-    const f3 wp = c.wp, nrm = c.nrm, cur = c.cur;
-    float pfx = (float)c.px, pfy = (float)c.py;
-    uint8_t accept = 0;
-    float alpha = 1.f;
-    f3 prev{0.f, 0.f, 0.f};
-    float sample_spp = 0.f;
-    o.prev_f = f3{0.f, 0.f, 0.f};
-    o.alpha_f = 1.f;
-    o.prev_f_divided = false;
-    o.over = 0;
-    float tap_total = 0.f;
+    NoisyTaps tp;
+    tp.pfx = (float)c.px;
+    tp.pfy = (float)c.py;
+    tp.over = 0;
+    tp.inb = 0;
     if (frame > 0) {
+        const f3 wp = c.wp;
         const float* M = cam.m;
         float u = dot4(M[0], M[4], M[8], M[12], wp.x, wp.y, wp.z, 1.f);
         float v = dot4(M[1], M[5], M[9], M[13], wp.x, wp.y, wp.z, 1.f);
@@ -301,51 +303,76 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
         v = v + 1.f;
         u = u / 2.f;
         v = v / 2.f;
-        pfx = u * (float)P.width - cam.jx;
-        pfy = v * (float)P.height - (1 - cam.jy);
+        const float pfx = u * (float)P.width - cam.jx;
+        const float pfy = v * (float)P.height - (1 - cam.jy);
+        tp.pfx = pfx;
+        tp.pfy = pfy;
         const float flx = floorf(pfx), fly = floorf(pfy);
         // Clamp before converting: a far-off reprojection must not overflow int.
         const int ix = (int)fminf(fmaxf(flx, -2.f), (float)P.width + 1.f);
         const int iy = (int)fminf(fmaxf(fly, -2.f), (float)P.height + 1.f);
         const float fx = pfx - flx, fy = pfy - fly;
         const float omx = 1.f - fx, omy = 1.f - fy;
-        const float wts[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
+        tp.wts[0] = omx * omy;
+        tp.wts[1] = fx * omy;
+        tp.wts[2] = omx * fy;
+        tp.wts[3] = fx * fy;
         if (P.check_reach) {  // the in-image taps span [x0, x1] x [y0, y1]
             const int x0 = max(ix, 0), x1 = min(ix + 1, P.width - 1);
             const int y0 = max(iy, 0), y1 = min(iy + 1, P.height - 1);
             if (x0 <= x1 && y0 <= y1)
-                o.over = max(max(max(P.vx0 - x0, x1 - (P.vx1 - 1)), max(P.vy0 - y0, y1 - (P.vy1 - 1))), 0);
+                tp.over = max(max(max(P.vx0 - x0, x1 - (P.vx1 - 1)), max(P.vy0 - y0, y1 - (P.vy1 - 1))), 0);
         }
-        f3 pp[4], pn[4], pc[4], pa[4];
-        float sp[4];
-        bool inb[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int sx = ix + (i & 1), sy = iy + (i >> 1);
-            inb[i] = sx >= 0 && sy >= 0 && sx < P.width && sy < P.height;
+            tp.inb |= (uint32_t)(sx >= 0 && sy >= 0 && sx < P.width && sy < P.height) << i;
             const long s = pix(P, clamp_rx(P, sx), clamp_ry(P, sy));
-            pp[i] = ld3in<IN>(in.p_prev, s);
-            pn[i] = ld3in<IN>(in.n_prev, s);
-            pc[i] = ld3(in.noisy_prev, s);
-            sp[i] = (float)in.spp_prev[s];
-            if (FILT) pa[i] = ld3(acc_prev, s);  // same taps (bmfr.cl:801-832)
+            tp.pp[i] = ld3in<IN>(in.p_prev, s);
+            tp.pn[i] = ld3in<IN>(in.n_prev, s);
+            tp.pc[i] = ld3(in.noisy_prev, s);
+            tp.sp[i] = (float)in.spp_prev[s];
+            if (FILT) tp.pa[i] = ld3(acc_prev, s);  // same taps (bmfr.cl:801-832)
         }
+    }
+    return tp;
+}
+
+template <bool FILT = false>
+__device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const NoisyCur& c, const NoisyTaps& tp,
+                                                      int frame) {
+    NoisyItem o;
+    o.owner = c.owner;
+    o.lin = pix(P, c.px, c.py);
+    o.n = c.nrm;
+    o.p = c.wp;
+    const f3 wp = c.wp, nrm = c.nrm, cur = c.cur;
+    uint8_t accept = 0;
+    float alpha = 1.f;
+    f3 prev{0.f, 0.f, 0.f};
+    float sample_spp = 0.f;
+    o.prev_f = f3{0.f, 0.f, 0.f};
+    o.alpha_f = 1.f;
+    o.prev_f_divided = false;
+    o.over = tp.over;
+    float tap_total = 0.f;
+    if (frame > 0) {
         float total = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {  // bmfr.cl:374-419
-            const f3 d{pp[i].x - wp.x, pp[i].y - wp.y, pp[i].z - wp.z};
-            const f3 dn{pn[i].x - nrm.x, pn[i].y - nrm.y, pn[i].z - nrm.z};
-            if (inb[i] && dot3(d, d) < P.position_limit_sq && dot3(dn, dn) < P.normal_limit_sq) {
+            const f3 d{tp.pp[i].x - wp.x, tp.pp[i].y - wp.y, tp.pp[i].z - wp.z};
+            const f3 dn{tp.pn[i].x - nrm.x, tp.pn[i].y - nrm.y, tp.pn[i].z - nrm.z};
+            if ((tp.inb & (1u << i)) && dot3(d, d) < P.position_limit_sq && dot3(dn, dn) < P.normal_limit_sq) {
                 accept |= (uint8_t)(1 << i);
-                sample_spp = sample_spp + wts[i] * sp[i];
-                prev.x = prev.x + wts[i] * pc[i].x;
-                prev.y = prev.y + wts[i] * pc[i].y;
-                prev.z = prev.z + wts[i] * pc[i].z;
-                total = total + wts[i];
+                sample_spp = sample_spp + tp.wts[i] * tp.sp[i];
+                prev.x = prev.x + tp.wts[i] * tp.pc[i].x;
+                prev.y = prev.y + tp.wts[i] * tp.pc[i].y;
+                prev.z = prev.z + tp.wts[i] * tp.pc[i].z;
+                total = total + tp.wts[i];
                 if (FILT) {  // accumulate_filtered_data's sums: same weights, same order
-                    o.prev_f.x = o.prev_f.x + wts[i] * pa[i].x;
-                    o.prev_f.y = o.prev_f.y + wts[i] * pa[i].y;
-                    o.prev_f.z = o.prev_f.z + wts[i] * pa[i].z;
+                    o.prev_f.x = o.prev_f.x + tp.wts[i] * tp.pa[i].x;
+                    o.prev_f.y = o.prev_f.y + tp.wts[i] * tp.pa[i].y;
+                    o.prev_f.z = o.prev_f.z + tp.wts[i] * tp.pa[i].z;
                 }
             }
         }
@@ -372,11 +399,18 @@ __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const Nois
     }
     const float beta = 1.f - alpha;
     o.color = f3{alpha * cur.x + beta * prev.x, alpha * cur.y + beta * prev.y, alpha * cur.z + beta * prev.z};
-    o.pfx = pfx;
-    o.pfy = pfy;
+    o.pfx = tp.pfx;
+    o.pfy = tp.pfy;
     o.accept = accept;
     o.spp = new_spp;
     return o;
+}
+
+template <bool FILT = false, class IN = float>
+__device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const NoisyInputs& in, const Camera& cam,
+                                                     const NoisyCur& c, int frame,
+                                                     const float* __restrict__ acc_prev = nullptr) {
+    return noisy_taps_finish<FILT>(P, c, noisy_taps_issue<FILT, IN>(P, in, cam, c, frame, acc_prev), frame);
 }
 
 // One work-group's reprojection-reach report (tiled contexts): the lanes
