@@ -6,8 +6,8 @@
   prof_summary.py calib <dir> <counter> <bytes>   counter / true bytes per calibration kernel
   prof_summary.py traffic <fetch_dir> <write_dir> <workload> <pixels> <alg_bytes_per_px>
                                        -> profiles/pmc_k1.json entry (HBM bytes per K1 launch)
-  prof_summary.py sq <dir> [<dir> ...] -> profiles/r01_sq_counters.json (K1 / K2 per-launch
-                                       means of every counter in the passes, plus derived rates)
+  prof_summary.py sq <out.json> <dir> [<dir> ...] -> K1 / K2 per-launch means of every counter
+                                       in the passes, plus derived rates
 
 FETCH_SIZE / WRITE_SIZE are KB per dispatch (rocprofv3 derived counters).
 MI355X_MICROARCH.md (HBM): on gfx950 FETCH_SIZE reads half the bytes of a
@@ -65,7 +65,7 @@ def pmc(d, counter):
     return {k: statistics.mean(v) for k, v in per.items()}
 
 
-KERNELS = {"K1 k_fused_cols": "k_fused_cols<4, 6, float, false>", "K2 k_fused_taa": "k_fused_taa<true, float>"}
+KERNELS = {"K1 k_fused_cols": "k_fused_cols<4, 6, float>", "K2 k_fused_taa": "k_fused_taa<float>"}
 
 
 def sq(dirs):
@@ -82,6 +82,11 @@ def sq(dirs):
             e["valu_instr_per_simd"] = round(e["SQ_INSTS_VALU"] / 1024, 3)  # 256 CUs x 4 SIMDs
         if "SQ_WAIT_ANY" in e and "SQ_WAVE_CYCLES" in e:
             e["wait_any_frac_of_wave_cycles"] = round(e["SQ_WAIT_ANY"] / e["SQ_WAVE_CYCLES"], 3)
+        for k in ("SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+            if k in e and "SQ_WAVE_CYCLES" in e:
+                e[k.lower() + "_frac_of_wave_cycles"] = round(e[k] / e["SQ_WAVE_CYCLES"], 3)
+        if "SQC_ICACHE_MISSES" in e and "SQC_ICACHE_HITS" in e:
+            e["icache_miss_rate"] = round(e["SQC_ICACHE_MISSES"] / (e["SQC_ICACHE_MISSES"] + e["SQC_ICACHE_HITS"]), 4)
         if "GRBM_GUI_ACTIVE" in e:
             e["kernel_cycles_per_xcd"] = round(e["GRBM_GUI_ACTIVE"] / 8, 3)
             if "TA_BUSY_avr" in e:
@@ -101,9 +106,8 @@ def main():
         for k, v in pmc(sys.argv[2], sys.argv[3]).items():
             print(f"{k:40s} {sys.argv[3]} {v:12.0f} KB  counted/true {v / true_kb:.3f}")
     elif cmd == "sq":
-        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                            "r01_sq_counters.json")
-        d = sq(sys.argv[2:])
+        path = sys.argv[2]
+        d = sq(sys.argv[3:])
         json.dump(d, open(path, "w"), indent=1)
         print(json.dumps(d, indent=1))
     elif cmd == "traffic":
