@@ -102,6 +102,10 @@ bmfr_status validate(const bmfr_config* c) {
         const int workset = E * ((n + E - 1) / E);
         if (n < E || workset + 30 > 2 * n) return BMFR_ERROR_INVALID_ARGUMENT;
     }
+    // Kernels address plane elements at 32-bit byte offsets (ld3/st3 in
+    // bmfr_device.h): the widest per-pixel element is 12 bytes.
+    if ((unsigned long long)c->image_width * c->image_height * 12ull > 0xffffffffull)
+        return BMFR_ERROR_INVALID_ARGUMENT;
     if (c->features_not_scaled < 0 || c->features_scaled < 0 ||
         c->features_not_scaled + c->features_scaled > BMFR_MAX_FEATURES ||
         c->features_not_scaled + c->features_scaled < 1)

@@ -29,12 +29,35 @@ struct f3 {
 struct __attribute__((packed, aligned(4))) f3mem {
     float x, y, z;
 };
-__device__ __forceinline__ f3 ld3(const float* __restrict__ b, long i) {
-    const f3mem v = *reinterpret_cast<const f3mem*>(b + 3 * i);
+
+// Plane elements by pixel index i.  The address is the plane's base (a kernel
+// argument: uniform, in SGPRs) plus a 32-bit byte offset (one VGPR) -- the
+// SGPR-base form of the global memory instructions -- so the planes read at
+// one pixel share a single offset register and no 64-bit address arithmetic
+// is spent per access.  Every plane is under 4 GiB (validate() in
+// bmfr_capi.hip bounds the image), so i * element size fits 32 bits.
+template <class T>
+__device__ __forceinline__ const T* at_byte(const T* b, uint32_t off) {
+    return reinterpret_cast<const T*>(reinterpret_cast<const char*>(b) + off);
+}
+template <class T>
+__device__ __forceinline__ T* at_byte(T* b, uint32_t off) {
+    return reinterpret_cast<T*>(reinterpret_cast<char*>(b) + off);
+}
+template <class T>
+__device__ __forceinline__ T ld_px(const T* b, uint32_t i) {
+    return *at_byte(b, i * (uint32_t)sizeof(T));
+}
+template <class T>
+__device__ __forceinline__ void st_px(T* b, uint32_t i, T v) {
+    *at_byte(b, i * (uint32_t)sizeof(T)) = v;
+}
+__device__ __forceinline__ f3 ld3(const float* __restrict__ b, uint32_t i) {
+    const f3mem v = *reinterpret_cast<const f3mem*>(at_byte(b, i * 12u));
     return f3{v.x, v.y, v.z};
 }
-__device__ __forceinline__ void st3(float* __restrict__ b, long i, f3 v) {
-    *reinterpret_cast<f3mem*>(b + 3 * i) = f3mem{v.x, v.y, v.z};
+__device__ __forceinline__ void st3(float* __restrict__ b, uint32_t i, f3 v) {
+    *reinterpret_cast<f3mem*>(at_byte(b, i * 12u)) = f3mem{v.x, v.y, v.z};
 }
 
 // One pixel of an input plane of element type IN (float: the reference's
@@ -43,9 +66,9 @@ struct __attribute__((packed, aligned(2))) h3mem {
     _Float16 x, y, z;
 };
 template <class IN>
-__device__ __forceinline__ f3 ld3in(const float* __restrict__ b, long i) {
+__device__ __forceinline__ f3 ld3in(const float* __restrict__ b, uint32_t i) {
     if constexpr (sizeof(IN) == 2) {
-        const h3mem v = reinterpret_cast<const h3mem*>(b)[i];
+        const h3mem v = *reinterpret_cast<const h3mem*>(at_byte(b, i * 6u));
         return f3{(float)v.x, (float)v.y, (float)v.z};
     } else {
         return ld3(b, i);

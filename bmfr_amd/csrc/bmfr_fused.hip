@@ -329,8 +329,8 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
         else state_hi |= bits << (16 * (s - 2));
         if (it.owner) {
             st3(A.noisy_out, it.lin, it.color);
-            A.spp_out[it.lin] = it.spp;
-            A.prev_pixel_out[it.lin] = make_float2(it.pfx, it.pfy);
+            st_px(A.spp_out, it.lin, it.spp);
+            st_px(A.prev_pixel_out, it.lin, make_float2(it.pfx, it.pfy));
         }
     }
     report_reach(P, A.reach, over);
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
     // the colours and the previous accumulation's taps.
     f3 n[kSubs], pos[kSubs];
     float2 pp[kSubs];
-    long lin[kSubs];
+    uint32_t lin[kSubs];
     uint32_t bits[kSubs];
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
         lin[s] = pix(P, (bits[s] & 1u) ? px : P.ox, (bits[s] & 1u) ? py : P.oy);
         n[s] = ld3in<IN>(in.n_cur, lin[s]);
         pos[s] = ld3in<IN>(in.p_cur, lin[s]);
-        pp[s] = A.prev_pixel_out[lin[s]];
+        pp[s] = ld_px(A.prev_pixel_out, lin[s]);
     }
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {

@@ -223,15 +223,21 @@ __device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const double* 
 // The polls are bounded (~2^20 sleeps): a scheduling bug would then give
 // wrong results instead of a wave that never finishes.
 constexpr int kMaxPolls = 1 << 20;
+#ifndef BMFR_POLL_SLEEP
+#define BMFR_POLL_SLEEP 1
+#endif
+#ifndef BMFR_PIVOT_PRIO
+#define BMFR_PIVOT_PRIO 0
+#endif
 __device__ __forceinline__ void wait_pub(const int* pub, int c) {
     for (int k = 0; k < kMaxPolls && __hip_atomic_load(pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c; ++k)
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(BMFR_POLL_SLEEP);
 }
 __device__ __forceinline__ void wait_all_progress(const int* prog, int c) {
     for (int w = 0; w < 4; ++w)
         for (int k = 0;
              k < kMaxPolls && __hip_atomic_load(&prog[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c; ++k)
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(BMFR_POLL_SLEEP);
 }
 
 // The owner of pivot column c (>= 1), once steps 0..c-1 are applied to it:
@@ -337,8 +343,10 @@ struct WaveFit {
                 const float ulen2 = L.piv[c % kUBufs][0], recip = L.piv[c % kUBufs][1];
                 if constexpr (nxt < NF) {
                     if (publish) {  // the next pivot is every wave's critical path: issue it first
+                        if (BMFR_PIVOT_PRIO) __builtin_amdgcn_s_setprio(BMFR_PIVOT_PRIO);
                         update_column<c>(a[slot(nxt)], u, ulen2, recip, l);
                         publish_pivot<nxt, B>(a[slot(nxt)], L, l);
+                        if (BMFR_PIVOT_PRIO) __builtin_amdgcn_s_setprio(0);
                     }
                 }
                 sfor<NSL>([&](auto K) {
@@ -536,8 +544,8 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
             L.keep[i][2][t] = it.prev_f.z;
             if (it.owner) {
                 st3(A.noisy_out, it.lin, it.color);
-                A.spp_out[it.lin] = it.spp;
-                A.prev_pixel_out[it.lin] = make_float2(it.pfx, it.pfy);
+                st_px(A.spp_out, it.lin, it.spp);
+                st_px(A.prev_pixel_out, it.lin, make_float2(it.pfx, it.pfy));
             }
             if (i & 1) {  // rows j = 4w + i - 1, 4w + i: adjacent halves of lane l's row slot
                 // (pair 2w + i/2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)
@@ -563,7 +571,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     int l3 = l;  // opaque copy: recompute phase-1 addresses instead of keeping them live across the fit
     asm volatile("" : "+v"(l3));
     const int2 off = kBlockOffsets[frame & 15];
-    long lin[4];
+    uint32_t lin[4];
     f3 nrm[4], wp[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

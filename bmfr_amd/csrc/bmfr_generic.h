@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_fused_block(Params P, NoisyInputs in, C
     float a[B][kSubs];
     f3 n_keep[kSubs], p_keep[kSubs];
     float pfx[kSubs], pfy[kSubs];
-    long lin[kSubs];
+    uint32_t lin[kSubs];
     uint32_t flags = 0;  // per s: bit 8s owner, bits 8s+1.. accept(4)
     uint32_t spps = 0;
 #pragma unroll

@@ -80,7 +80,7 @@ struct NoisyItem {
     f3 n, p;          // current normal / world position of the (mirrored) pixel
     f3 color;         // blended colour (features B-3..B-1)
     float pfx, pfy;   // prev_frame_pixel_f
-    long lin;         // linear (mirrored) pixel
+    uint32_t lin;     // linear (mirrored) pixel
     uint8_t accept;
     uint8_t spp;
     bool owner;       // pixel_without_mirror inside the image
@@ -152,8 +152,8 @@ __device__ __forceinline__ void k1_block(const Params& P, int g, int& bx, int& b
 
 // Linear index of image pixel (x, y) in a plane of the buffer region, and
 // clamps into the region (= the image when untiled).
-__device__ __forceinline__ long pix(const Params& P, int x, int y) {
-    return (long)(y - P.oy) * P.stride + (x - P.ox);
+__device__ __forceinline__ uint32_t pix(const Params& P, int x, int y) {
+    return (uint32_t)((y - P.oy) * P.stride + (x - P.ox));
 }
 __device__ __forceinline__ int clamp_rx(const Params& P, int x) { return min(max(x, P.ox), P.ox + P.stride - 1); }
 __device__ __forceinline__ int clamp_ry(const Params& P, int y) { return min(max(y, P.oy), P.oy + P.rows - 1); }
@@ -165,7 +165,7 @@ __device__ __forceinline__ NoisyItem noisy_item(const Params& P, const NoisyInpu
     const int ux = gx - kEdge / 2 + off.x, uy = gy - kEdge / 2 + off.y;
     const int px = mirror(ux, P.width), py = mirror(uy, P.height);
     o.owner = ux >= 0 && ux < P.width && uy >= 0 && uy < P.height;
-    o.lin = (long)py * P.width + px;
+    o.lin = (uint32_t)(py * P.width + px);
 
     const f3 wp = ld3(in.p_cur, o.lin);
     const f3 nrm = ld3(in.n_cur, o.lin);
@@ -203,7 +203,7 @@ __device__ __forceinline__ NoisyItem noisy_item(const Params& P, const NoisyInpu
         for (int i = 0; i < 4; ++i) {  // bmfr.cl:374-419
             const int sx = ix + (i & 1), sy = iy + (i >> 1);
             if (sx >= 0 && sy >= 0 && sx < P.width && sy < P.height) {
-                const long s = (long)sy * P.width + sx;
+                const uint32_t s = (uint32_t)(sy * P.width + sx);
                 const f3 pp = ld3(in.p_prev, s);
                 const f3 d{pp.x - wp.x, pp.y - wp.y, pp.z - wp.z};
                 if (dot3(d, d) < P.position_limit_sq) {
@@ -211,7 +211,7 @@ __device__ __forceinline__ NoisyItem noisy_item(const Params& P, const NoisyInpu
                     const f3 dn{pn.x - nrm.x, pn.y - nrm.y, pn.z - nrm.z};
                     if (dot3(dn, dn) < P.normal_limit_sq) {
                         accept |= (uint8_t)(1 << i);
-                        sample_spp = sample_spp + wts[i] * (float)in.spp_prev[s];
+                        sample_spp = sample_spp + wts[i] * (float)ld_px(in.spp_prev, s);
                         const f3 pc = ld3(in.noisy_prev, s);
                         prev.x = prev.x + wts[i] * pc.x;
                         prev.y = prev.y + wts[i] * pc.y;
@@ -262,7 +262,7 @@ __device__ __forceinline__ NoisyCur noisy_load_current(const Params& P, const No
     c.px = mirror(ux, P.width);
     c.py = mirror(uy, P.height);
     c.owner = ux >= 0 && ux < P.width && uy >= 0 && uy < P.height;
-    const long lin = pix(P, c.px, c.py);
+    const uint32_t lin = pix(P, c.px, c.py);
     c.wp = ld3in<IN>(in.p_cur, lin);
     c.nrm = ld3in<IN>(in.n_cur, lin);
     c.cur = ld3in<IN>(in.noisy_cur, lin);
@@ -327,11 +327,11 @@ __device__ __forceinline__ NoisyTaps noisy_taps_issue(const Params& P, const Noi
         for (int i = 0; i < 4; ++i) {
             const int sx = ix + (i & 1), sy = iy + (i >> 1);
             tp.inb |= (uint32_t)(sx >= 0 && sy >= 0 && sx < P.width && sy < P.height) << i;
-            const long s = pix(P, clamp_rx(P, sx), clamp_ry(P, sy));
+            const uint32_t s = pix(P, clamp_rx(P, sx), clamp_ry(P, sy));
             tp.pp[i] = ld3in<IN>(in.p_prev, s);
             tp.pn[i] = ld3in<IN>(in.n_prev, s);
             tp.pc[i] = ld3(in.noisy_prev, s);
-            tp.sp[i] = (float)in.spp_prev[s];
+            tp.sp[i] = (float)ld_px(in.spp_prev, s);
             if (FILT) tp.pa[i] = ld3(acc_prev, s);  // same taps (bmfr.cl:801-832)
         }
     }

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_weighted_sum(Params P, const float* __r
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
     if (x >= P.width || y >= P.height) return;
-    const long lin = (long)y * P.width + x;
+    const uint32_t lin = (uint32_t)(y * P.width + x);
     const int g = block_of_pixel(P, x, y, frame);
     const f3 c = weighted_color(P, weights + (size_t)g * (P.buffers - 3) * 3,
                                 mins_maxs + (size_t)g * P.scaled * 2, ld3(normals, lin),
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void k_accumulate_filtered(
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
     if (x >= P.width || y >= P.height) return;
-    const long lin = (long)y * P.width + x;
+    const uint32_t lin = (uint32_t)(y * P.width + x);
     const float2 pp = prev_pixel[lin];
     const f3 a = blend_filtered(P, ld3(filtered, lin), pp.x, pp.y, frame > 0 ? accept[lin] : 0, spp[lin],
                                 acc_prev, frame);
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
     if (x >= P.width || y >= P.height) return;
-    const long lin = (long)y * P.width + x;
+    const uint32_t lin = (uint32_t)(y * P.width + x);
     const f3 me = ld3(new_frame, lin);
     const float2 pf = prev_pixel[lin];
     f3 pc[4], nb[9];

@@ -53,7 +53,7 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
     float2 pf[KN];
 #pragma unroll
     for (int k = 0; k < KN; ++k)
-        pf[k] = T.prev_pixel[pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + ty + 4 * k, P.ty1 - 1))];
+        pf[k] = ld_px(T.prev_pixel, pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + ty + 4 * k, P.ty1 - 1)));
     f3 v[KN + 1], al[KN + 1];
     int hx = 0, hy = 0;  // this thread's ring pixel (t < RING), in tile + halo coordinates
     if (t < 2 * HW) {
@@ -70,7 +70,7 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
         // Clamped into the buffer region (= the image when untiled): a tile
         // whose last 64-px column or TH-row band overhangs its output reads
         // no pixel outside the region; such values reach no output pixel.
-        const long lin = pix(P, clamp_rx(P, x0 - 1 + lx), clamp_ry(P, y0 - 1 + ly));
+        const uint32_t lin = pix(P, clamp_rx(P, x0 - 1 + lx), clamp_ry(P, y0 - 1 + ly));
         v[k] = ld3(T.src, lin);
         al[k] = ld3in<IN>(T.albedo, lin);
     }
