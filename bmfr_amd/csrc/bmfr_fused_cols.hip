@@ -223,21 +223,15 @@ __device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const double* 
 // The polls are bounded (~2^20 sleeps): a scheduling bug would then give
 // wrong results instead of a wave that never finishes.
 constexpr int kMaxPolls = 1 << 20;
-#ifndef BMFR_POLL_SLEEP
-#define BMFR_POLL_SLEEP 1
-#endif
-#ifndef BMFR_PIVOT_PRIO
-#define BMFR_PIVOT_PRIO 0
-#endif
 __device__ __forceinline__ void wait_pub(const int* pub, int c) {
     for (int k = 0; k < kMaxPolls && __hip_atomic_load(pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c; ++k)
-        __builtin_amdgcn_s_sleep(BMFR_POLL_SLEEP);
+        __builtin_amdgcn_s_sleep(1);
 }
 __device__ __forceinline__ void wait_all_progress(const int* prog, int c) {
     for (int w = 0; w < 4; ++w)
         for (int k = 0;
              k < kMaxPolls && __hip_atomic_load(&prog[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c; ++k)
-            __builtin_amdgcn_s_sleep(BMFR_POLL_SLEEP);
+            __builtin_amdgcn_s_sleep(1);
 }
 
 // The owner of pivot column c (>= 1), once steps 0..c-1 are applied to it:
@@ -343,10 +337,8 @@ struct WaveFit {
                 const float ulen2 = L.piv[c % kUBufs][0], recip = L.piv[c % kUBufs][1];
                 if constexpr (nxt < NF) {
                     if (publish) {  // the next pivot is every wave's critical path: issue it first
-                        if (BMFR_PIVOT_PRIO) __builtin_amdgcn_s_setprio(BMFR_PIVOT_PRIO);
                         update_column<c>(a[slot(nxt)], u, ulen2, recip, l);
                         publish_pivot<nxt, B>(a[slot(nxt)], L, l);
-                        if (BMFR_PIVOT_PRIO) __builtin_amdgcn_s_setprio(0);
                     }
                 }
                 sfor<NSL>([&](auto K) {
