@@ -662,7 +662,7 @@ __global__ __launch_bounds__(kThreads, kColsWaves) void k_fused_cols(Params P, K
 // runs the tiles in K1's tail, where its last work-groups leave CUs idle, and
 // a frame costs one launch.  K2 of f - 1 reads frame f - 1's state, which K1
 // of f does not write (double-buffered), and frame f - 2's TAA output.
-constexpr int kSeqTaaH = 8;
+constexpr int kSeqTaaH = 12;
 template <int NS, int FS, class IN>
 __global__ __launch_bounds__(kThreads, 4) void k_fused_cols_taa(Params P, K1Args A, Params P2, TaaArgs T, int nk1,
                                                                 int nk1p) {

@@ -107,8 +107,10 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
 
 // --------------------------------------------------------- fused K2: TAA --
 // Tone map + TAA, one 64 x kTaaH tile per 256-thread work-group (taa_tile,
-// bmfr_taa_tile.h); 64x16: 22 KB of LDS per work-group.
-constexpr int kTaaW = 64, kTaaH = 16;
+// bmfr_taa_tile.h).
+// Tile height measured at 4K (K2 ms): 8: 0.114, 12: 0.105, 16: 0.112,
+// 24: 0.130, 32: 0.135; forcing 4 waves/SIMD (128 VGPRs) at 16: 0.159.
+constexpr int kTaaW = 64, kTaaH = 12;
 template <class IN>
 __global__ __launch_bounds__(256) void k_fused_taa(Params P, TaaArgs T) {
     __shared__ float4 Y[(kTaaW + 2) * (kTaaH + 2)];  // YCoCg (+ pad): one 16-byte read per neighbour
