@@ -13,7 +13,11 @@ active on every timed frame).
 
 The N = 1 line also carries the metric's other sizes, untiled on the same
 GPU: `ms_per_frame_1080p` (1920x1080) and `ms_per_frame_8k` (7680x4320, the
-1-GPU point of the north star's scaling target).
+1-GPU point of the north star's scaling target), and
+`ms_per_frame_sequence`: the same 4K frames through bmfr_process_sequence
+(K2 of frame f inside K1 of f + 1's launch, as the reference's frame loop
+enqueues every frame without waiting).  `value` stays the per-frame API's
+number (bmfr_process_frame: each frame's output complete at its return).
 
 Multi-GPU (torchrun, one process per GPU): BASELINE config 4 -- one
 7680x4320 frame cut into a tile grid (2x1, 2x2, 4x2 for N = 2, 4, 8), one
@@ -32,7 +36,8 @@ events around the kernels of every 10th timed frame (libbmfr's profiling
 stride), recorded on the stream the kernels run on; the other timed frames
 run without events.
 
-Extra JSON fields: `roofline` for the dominant kernel (K1); `cpu_baseline` = the CPU oracle
+Extra JSON fields: `roofline` for the dominant kernel (K1), `roofline_k2` for
+the TAA kernel (compulsory bytes: bench.k2_bytes_per_px); `cpu_baseline` = the CPU oracle
 (oracle/liboracle.so, OpenMP) on a bounded sample of the same sequence.
 """
 from __future__ import annotations
@@ -66,6 +71,13 @@ def k1_bytes_per_px(s: int) -> int:
     return 15 * s + 50
 
 
+def k2_bytes_per_px(s: int) -> int:
+    """K2's compulsory bytes: albedo (3s) + previous TAA output (12) + output
+    (12); the accumulated filtered colour and the reprojected positions it
+    reads are K1's intermediates (their bytes are not compulsory)."""
+    return 3 * s + 24
+
+
 def frame_bytes_per_px(s: int) -> int:
     """K1's plus K2's: albedo (3s) + previous TAA output (12) + output (12)."""
     return 18 * s + 74
@@ -86,6 +98,7 @@ def parse():
                     help="tone map with the device library's powr (bit-identical to the reference kernel "
                          "on gfx950) instead of the correctly rounded one")
     ap.add_argument("--no-1080p", action="store_true", help="skip the 1920x1080 line (N = 1 only)")
+    ap.add_argument("--no-sequence", action="store_true", help="skip the sequence-mode field of the N = 1 line")
     ap.add_argument("--no-8k", action="store_true", help="skip the untiled 7680x4320 line (N = 1) / the 1-GPU "
                                                          "reference time (N > 1)")
     ap.add_argument("--frames-8k", type=int, default=30, help="timed frames of the untiled 8K line (N = 1)")
@@ -293,8 +306,10 @@ def valu_roofline():
     the same bench command (profiles/*sq_counters.json, newest round):
     K1's VALU instructions per SIMD x the achievable issue cost of a wave64
     f32 instruction (3.24 cycles, profiles/r01_valu_rate.txt) / K1's cycles.
-    K1 runs below both roofs -- its limiter is the latency of phase 1's
-    dependent gathers and the fit's per-column barriers."""
+    The guide's nominal issue rate (2 cycles, MI355X_MICROARCH.md) gives
+    `valu_frac_nominal`.  K1 runs below both roofs -- its limiter is the
+    latency of phase 1's dependent gathers and of the fit's pivot chain
+    (DESIGN.md section 5)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_sq_counters.json")))
     if not files:
@@ -305,7 +320,8 @@ def valu_roofline():
     if not c:
         return {}
     return {"valu_frac": round(c["valu_instr_per_simd"] * 3.24 / c["kernel_cycles_per_xcd"], 3),
-            "limiter": "latency (phase-1 gathers, per-column barriers) under the HBM and VALU roofs",
+            "valu_frac_nominal": round(c["valu_instr_per_simd"] * 2.0 / c["kernel_cycles_per_xcd"], 3),
+            "limiter": "latency (phase-1 gathers, the fit's pivot chain) under the HBM and VALU roofs",
             "valu_source": os.path.relpath(files[-1], ROOT) + ": SQ_INSTS_VALU / GRBM_GUI_ACTIVE, "
                                                                 "3.24 cycles per wave64 VALU instruction"}
 
@@ -354,7 +370,12 @@ def main():
     cfg = r["cfg"]
     # The metric's other resolutions (BASELINE.json: ms/frame @1080p & 4K, and
     # the 8K frame of the scaling target), single GPU only.
-    r1080 = r8k = None
+    r1080 = r8k = rseq = None
+    # The same frames as one bmfr_process_sequence call per 64 frames (K2 of
+    # frame f in K1 of f + 1's tail): the reference's own frame loop
+    # (bmfr.cpp:417-485) enqueues every frame without waiting, as this does.
+    if world == 1 and not a.sequence and not a.no_sequence:
+        rseq = run_sequence(a, W, H, (0, 0, W, H), None, 0, 1, dev, backend, a.steps, a.warmup, per_frame=False)
     if world == 1 and not a.no_1080p and (W, H) != (1920, 1080):
         r1080 = run_sequence(a, 1920, 1080, (0, 0, 1920, 1080), None, 0, 1, dev, backend, a.steps, a.warmup,
                              per_frame=not a.sequence)
@@ -413,6 +434,14 @@ def main():
         }
         if world == 1:
             line["roofline"].update(valu_roofline())
+        if world == 1:
+            k2 = k2_bytes_per_px(s) * tile_px / (r["k2_ms"] * 1e-3) / 1e9 if not a.sequence else None
+            if k2:
+                line["roofline_k2"] = {"bound": "hbm", "achieved": round(k2, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                       "frac": round(k2 / HBM_PEAK_GBS, 4), "kernel": "k_fused_taa (K2)",
+                                       "algorithmic_bytes_per_launch": k2_bytes_per_px(s) * tile_px}
+        if rseq is not None:
+            line["ms_per_frame_sequence"] = side_line(rseq)
         if r1080 is not None:
             line["ms_per_frame_1080p"] = side_line(r1080)
         if r8k is not None:
