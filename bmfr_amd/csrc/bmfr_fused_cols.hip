@@ -524,8 +524,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 float v;
                 if (f < B - 3) v = feature_value(f, it.n, it.p);
                 else v = f == B - 3 ? it.color.x : (f == B - 2 ? it.color.y : it.color.z);
-                if (__builtin_isnan(v)) v = 0.0f;              // bmfr.cl:468-469
-                v = fmaxf(fminf(v, 65504.f), -65504.f);         // bmfr.cl:471-473
+                // NaN -> 0 (bmfr.cl:468-469), then the +-65504 clamp (bmfr.cl:471-473)
+                // as one med3 (equal to fmax(fmin(v, 65504), -65504) for every non-NaN v)
+                v = __builtin_isnan(v) ? 0.0f : __builtin_amdgcn_fmed3f(v, -65504.f, 65504.f);
                 pk[f][i & 1] = (_Float16)v;
             }
             spps |= (uint32_t)it.spp << (8 * i);

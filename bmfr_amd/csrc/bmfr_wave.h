@@ -24,6 +24,10 @@ __device__ __forceinline__ void lds_barrier() {
 __device__ __forceinline__ float dpp_shl8(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x108, 0xf, 0xf, true));
 }
+// lane l <- lane l-1 within its 16-lane row (valid for l % 16 > 0)
+__device__ __forceinline__ float dpp_shr1(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true));
+}
 // lanes 0..15 <- lanes 16..31 (permlane16_swap: odd rows of arg0 <-> even rows of arg1)
 __device__ __forceinline__ float swap16_down(float v) {
     const auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
@@ -52,10 +56,22 @@ __device__ __forceinline__ float wave_tree(float s) {
     } else {
         x = red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(s, a), b), c), d), e), f), h);
     }
-    float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+    // Step 4, ((x0 op x1) op x2) ... op x7 over lanes 0..7, as a serial DPP
+    // scan: after pass k, lane k holds the sum of x0..xk (one DPP op per pass,
+    // instead of a readlane + a scalar-operand op per term).
+    // (Sums only: a DPP-moved operand of fmaxf / fminf would first be
+    // canonicalised, one more instruction per pass.)
+    if constexpr (OP == RedOp::Sum) {
+        float r = x;
 #pragma unroll
-    for (int k = 1; k < 8; ++k) r = red<OP>(r, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), k)));
-    return r;
+        for (int k = 1; k < 8; ++k) r = dpp_shr1(r) + x;
+        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 7));
+    } else {
+        float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+#pragma unroll
+        for (int k = 1; k < 8; ++k) r = red<OP>(r, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), k)));
+        return r;
+    }
 }
 
 // Step 2 (256 -> 64, bmfr.cl:32-33 / 51-53 / 73-75) on the four partials of
