@@ -440,40 +440,59 @@ struct WaveFit {
     }
 };
 
-// Back substitution (bmfr.cl:658-699) in registers: lane (ch, x) of wave 0,
-// lane = 3 x + ch, holds column x of R for colour channel ch; the values a
-// step needs from other lanes come by readlane (3 per value, one per channel,
-// selected per lane), so there is no LDS round trip between the steps.  Every
-// element sees upstream's operations in upstream's order: row i divided by
-// the diagonal, the right-hand side reduced by the already-divided row
-// entries left to right, column i scaled by x_i.
+// Back substitution (bmfr.cl:658-699) in registers of wave 0, one 16-lane
+// DPP row per colour channel: lane 16 ch + x holds column x of R (rows
+// 0..RE-2) for channel ch.  Every cross-lane value a step needs moves inside
+// the row by DPP -- the diagonal by a row broadcast, the right-hand side's
+// serial reduction as a scan along the row -- so no step waits on a
+// readlane / scalar round trip.  Every element sees upstream's operations in
+// upstream's order: row i divided by the diagonal, the right-hand side
+// reduced by the already-divided row entries left to right, column i scaled
+// by x_i.
+template <int K>
+__device__ __forceinline__ float row_shl(float v) {  // lane l <- lane l + K of its row
+    if constexpr (K == 0) return v;
+    else return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x100 + K, 0xf, 0xf, true));
+}
+template <int N>
+__device__ __forceinline__ float row_bcast(float v) {  // every lane <- lane N of its row
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + N, 0xf, 0xf, false));
+}
 template <int B>
 __device__ __forceinline__ void back_substitute_regs(Lds<B>& L, int t) {
     constexpr int RE = B - 2;
+    static_assert(RE <= 16, "one DPP row per channel");
     if (t >= 64) return;
-    const int ch = t % 3, x = t / 3;
+    const int ch = t >> 4, x = t & 15;
+    const bool live = ch < 3 && x < RE;
     float col[RE - 1];  // rows 0..RE-2 of column x
 #pragma unroll
-    for (int y = 0; y < RE - 1; ++y) col[y] = x < RE ? L.R[(x * RE + y) * 3 + ch] : 0.f;
-    // value v of lane 3 X + ch, for this lane's channel
-    auto from = [&](float v, int X) {
-        const float a = lane_value(v, 3 * X), b = lane_value(v, 3 * X + 1), c = lane_value(v, 3 * X + 2);
-        return ch == 0 ? a : (ch == 1 ? b : c);
-    };
+    for (int y = 0; y < RE - 1; ++y) col[y] = live ? L.R[(x * RE + y) * 3 + ch] : 0.f;
+    sfor<RE - 1>([&](auto I) {
+        constexpr int i = RE - 2 - decltype(I)::value;
+        const float div = row_bcast<i>(col[i]);
+        if (live && x >= i) col[i] = col[i] / div;
+        const float v = col[i];
+        // x_i = ((rhs - v[i+1]) - v[i+2]) ... - v[RE-2], rhs = v[RE-1]: the
+        // running value walks from lane i+1 to lane RE-2 (src).
+        constexpr int src = i == RE - 2 ? RE - 1 : RE - 2;
+        float acc = v;
+        if constexpr (i < RE - 2) {
+            acc = row_shl<RE - 2 - i>(v) - v;  // lane i+1: rhs - v[i+1]
 #pragma unroll
-    for (int i = RE - 2; i >= 0; --i) {
-        const float div = from(col[i], i);
-        if (x < RE && x >= i) col[i] = col[i] / div;
-        float rhs = from(col[i], RE - 1);
-#pragma unroll
-        for (int j = i + 1; j < RE - 1; ++j) rhs = rhs - from(col[i], j);
-        if (x == RE - 1) col[i] = rhs;
-        if (x == i) {  // rhs is x_i on every lane of the channel
-#pragma unroll
-            for (int y = 0; y <= i; ++y) col[y] = col[y] * rhs;
+            for (int j = i + 2; j <= RE - 2; ++j) acc = dpp_shr1(acc) - v;  // lane j
         }
-    }
-    if (x == RE - 1) {
+        if constexpr (i < RE - 2) {
+            const float at_rhs = dpp_shr1(acc);  // lane RE-1 <- lane RE-2
+            if (x == RE - 1) col[i] = at_rhs;
+        }
+        const float xi = row_shl<src - i>(acc);  // lane i <- lane src
+        if (x == i) {
+#pragma unroll
+            for (int y = 0; y <= i; ++y) col[y] = col[y] * xi;
+        }
+    });
+    if (ch < 3 && x == RE - 1) {
 #pragma unroll
         for (int y = 0; y < B - 3; ++y) L.weights[y * 3 + ch] = col[y];
     }
