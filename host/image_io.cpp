@@ -1,4 +1,4 @@
-// image_io.cpp -- OpenEXR (scanline, NONE/RLE/ZIPS/ZIP) and PNG I/O over zlib.
+// image_io.cpp -- OpenEXR (scanline, NONE/RLE/ZIPS/ZIP/PIZ) and PNG I/O over zlib.
 // See image_io.h.  The EXR layout follows the published OpenEXR 2 file
 // format: magic + version, attribute list, per-chunk offset table, chunks of
 // (y, size, data) with each scanline's channels stored in channel-list order.
@@ -47,7 +47,8 @@ int lines_per_chunk(int compression) {
     switch (compression) {
         case BMFR_EXR_NONE: case BMFR_EXR_RLE: case BMFR_EXR_ZIPS: return 1;
         case BMFR_EXR_ZIP: return 16;
-        default: return 0;  // PIZ (4), PXR24 (5), B44 (6, 7), DWAA/B (8, 9): unsupported
+        case BMFR_EXR_PIZ: return 32;
+        default: return 0;  // PXR24 (5), B44 (6, 7), DWAA/B (8, 9): unsupported
     }
 }
 
@@ -208,12 +209,328 @@ bool rle_decode(const uint8_t* in, size_t n, std::vector<uint8_t>& out, size_t e
     return out.size() == expect;
 }
 
-bool decode_chunk(int compression, const uint8_t* data, size_t size, size_t raw_size, std::vector<uint8_t>& raw) {
+// ------------------------------------------------------------------ PIZ --
+// The published OpenEXR PIZ scheme, decoder side: a chunk of 32 scanlines is
+// held as 16-bit words, channel by channel (a FLOAT / UINT sample is two
+// words, low half first); the words went through (1) a range map onto
+// 0..maxValue given by a bitmap of the values present, (2) a 2-D Haar-like
+// wavelet per channel and word component (14-bit lifting when maxValue <
+// 2^14, modular 16-bit otherwise), (3) Huffman coding with a canonical code
+// whose 6-bit code lengths are stored run-length packed, plus one
+// pseudo-symbol that repeats the previous word.  Parity is unpinned: no
+// OpenEXR library and no reference PIZ file exist here; tests/exr_piz_py.py
+// is an independent encoder of the same scheme.
+namespace piz {
+
+constexpr int kUshortRange = 1 << 16;
+constexpr int kBitmapSize = kUshortRange >> 3;
+constexpr int kEncSize = (1 << 16) + 1;  // symbols 0..65535 + the run pseudo-symbol
+constexpr int kDecBits = 14;             // first-level decoding table index bits
+constexpr int kDecSize = 1 << kDecBits;
+constexpr int kShortZeroRun = 59, kLongZeroRun = 63;
+constexpr int kShortestLongRun = 2 + kLongZeroRun - kShortZeroRun;
+constexpr int kMaxCodeLength = 56;  // keeps every bit window inside 64 bits
+
+uint32_t rd32(const uint8_t* p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
+
+// Code lengths -> (length | code << 6), canonical: per length, consecutive
+// codes in symbol order; longer codes take the numerically lower values.
+void canonical_codes(std::vector<uint64_t>& hcode) {
+    uint64_t n[59] = {};
+    for (uint64_t l : hcode) ++n[l];
+    uint64_t c = 0;
+    for (int i = 58; i > 0; --i) {
+        const uint64_t nc = (c + n[i]) >> 1;
+        n[i] = c;
+        c = nc;
+    }
+    for (uint64_t& h : hcode)
+        if (h > 0) h = h | (n[h]++ << 6);
+}
+
+struct BitReader {
+    const uint8_t* p;
+    const uint8_t* end;
+    uint64_t c = 0;
+    int lc = 0;
+    bool byte() {
+        if (p >= end) return false;
+        c = (c << 8) | *p++;
+        lc += 8;
+        return true;
+    }
+    bool bits(int n, uint32_t& v) {
+        while (lc < n)
+            if (!byte()) return false;
+        lc -= n;
+        v = (uint32_t)((c >> lc) & ((1u << n) - 1));
+        return true;
+    }
+};
+
+// Packed code lengths of symbols im..iM (6 bits each; 59..62: a run of
+// 2..5 zero lengths; 63 + 8 bits: a run of 6..261).
+bool unpack_table(BitReader& in, uint32_t im, uint32_t iM, std::vector<uint64_t>& hcode) {
+    hcode.assign(kEncSize, 0);
+    for (uint32_t i = im; i <= iM; ++i) {
+        uint32_t l;
+        if (!in.bits(6, l)) return false;
+        if (l == (uint32_t)kLongZeroRun || l >= (uint32_t)kShortZeroRun) {
+            uint32_t run;
+            if (l == (uint32_t)kLongZeroRun) {
+                if (!in.bits(8, run)) return false;
+                run += kShortestLongRun;
+            } else {
+                run = l - kShortZeroRun + 2;
+            }
+            if ((uint64_t)i + run > (uint64_t)iM + 1) return false;
+            i += run - 1;  // the lengths are already zero
+        } else {
+            if (l > (uint32_t)kMaxCodeLength) return false;
+            hcode[i] = l;
+        }
+    }
+    canonical_codes(hcode);
+    return true;
+}
+
+struct DecEntry {
+    int len = 0;             // > 0: a code of this length (<= kDecBits) starts here
+    int sym = 0;             // its symbol
+    std::vector<int> longs;  // symbols of the longer codes with this prefix
+};
+
+bool build_decoder(const std::vector<uint64_t>& hcode, uint32_t im, uint32_t iM, std::vector<DecEntry>& dec) {
+    dec.assign(kDecSize, DecEntry{});
+    for (uint32_t i = im; i <= iM; ++i) {
+        const uint64_t c = hcode[i] >> 6;
+        const int l = (int)(hcode[i] & 63);
+        if (l == 0) continue;
+        if (c >> l) return false;  // not an l-bit code
+        if (l > kDecBits) {
+            DecEntry& e = dec[c >> (l - kDecBits)];
+            if (e.len) return false;
+            e.longs.push_back((int)i);
+        } else {
+            const uint64_t base = c << (kDecBits - l);
+            for (uint64_t k = 0; k < (1ull << (kDecBits - l)); ++k) {
+                DecEntry& e = dec[base + k];
+                if (e.len || !e.longs.empty()) return false;
+                e.len = l;
+                e.sym = (int)i;
+            }
+        }
+    }
+    return true;
+}
+
+// nbits bits of codes from in -> no words; symbol rlc repeats the previous
+// word (8-bit count).
+bool huf_decode(const std::vector<uint64_t>& hcode, const std::vector<DecEntry>& dec, const uint8_t* in,
+                const uint8_t* in_end, uint64_t nbits, int rlc, uint16_t* out, size_t no) {
+    BitReader r{in, in + (nbits + 7) / 8};
+    size_t o = 0;
+    auto emit = [&](int sym) -> bool {
+        if (sym == rlc) {
+            if (r.lc < 8) {  // the count may sit in the byte past the coded bits
+                if (r.p >= in_end) return false;
+                r.c = (r.c << 8) | *r.p++;
+                r.lc += 8;
+            }
+            r.lc -= 8;
+            const uint32_t cs = (uint32_t)(r.c >> r.lc) & 0xff;
+            if (o == 0 || o + cs > no) return false;
+            const uint16_t s = out[o - 1];
+            for (uint32_t k = 0; k < cs; ++k) out[o++] = s;
+            return true;
+        }
+        if (o >= no) return false;
+        out[o++] = (uint16_t)sym;
+        return true;
+    };
+    while (r.p < r.end) {
+        r.byte();
+        while (r.lc >= kDecBits) {
+            const DecEntry& e = dec[(r.c >> (r.lc - kDecBits)) & (kDecSize - 1)];
+            if (e.len) {
+                r.lc -= e.len;
+                if (!emit(e.sym)) return false;
+                continue;
+            }
+            bool found = false;
+            for (int sym : e.longs) {
+                const int l = (int)(hcode[sym] & 63);
+                while (r.lc < l && r.p < r.end) r.byte();
+                if (r.lc >= l && (hcode[sym] >> 6) == ((r.c >> (r.lc - l)) & ((1ull << l) - 1))) {
+                    r.lc -= l;
+                    if (!emit(sym)) return false;
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) return false;
+        }
+    }
+    // the last, short codes: drop the padding bits of the final byte
+    const int pad = (int)((8 - nbits) & 7);
+    if (pad > r.lc) return false;
+    r.c >>= pad;
+    r.lc -= pad;
+    while (r.lc > 0) {
+        const DecEntry& e = dec[(r.c << (kDecBits - r.lc)) & (kDecSize - 1)];
+        if (!e.len || e.len > r.lc) return false;
+        r.lc -= e.len;
+        if (!emit(e.sym)) return false;
+    }
+    return o == no;
+}
+
+bool huf_uncompress(const uint8_t* comp, size_t n, uint16_t* raw, size_t nraw) {
+    if (n == 0) return nraw == 0;
+    if (n < 20) return false;
+    const uint32_t im = rd32(comp), iM = rd32(comp + 4), nbits = rd32(comp + 12);
+    if (im >= (uint32_t)kEncSize || iM >= (uint32_t)kEncSize || im > iM) return false;
+    BitReader table{comp + 20, comp + n};
+    std::vector<uint64_t> hcode;
+    if (!unpack_table(table, im, iM, hcode)) return false;
+    const uint8_t* data = table.p;
+    if ((uint64_t)nbits > 8ull * (uint64_t)(comp + n - data)) return false;
+    std::vector<DecEntry> dec;
+    if (!build_decoder(hcode, im, iM, dec)) return false;
+    return huf_decode(hcode, dec, data, comp + n, nbits, (int)iM, raw, nraw);
+}
+
+// One level of the wavelet, inverse: 14-bit lifting or modular 16-bit.
+inline void wdec14(uint16_t l, uint16_t h, uint16_t& a, uint16_t& b) {
+    const int hi = (int16_t)h;
+    const int ai = (int16_t)l + (hi & 1) + (hi >> 1);
+    a = (uint16_t)(int16_t)ai;
+    b = (uint16_t)(int16_t)(ai - hi);
+}
+inline void wdec16(uint16_t l, uint16_t h, uint16_t& a, uint16_t& b) {
+    constexpr int kOff = 1 << 15, kMask = (1 << 16) - 1;
+    const int m = l, d = h;
+    const int bb = (m - (d >> 1)) & kMask;
+    const int aa = (d + bb - kOff) & kMask;
+    b = (uint16_t)bb;
+    a = (uint16_t)aa;
+}
+
+// Inverse 2-D wavelet of an nx x ny array of words at stride ox (x) and oy (y).
+void wav2_decode(uint16_t* in, int nx, int ox, int ny, int oy, uint16_t mx) {
+    const bool w14 = mx < (1 << 14);
+    auto dec = [w14](uint16_t l, uint16_t h, uint16_t& a, uint16_t& b) {
+        if (w14) wdec14(l, h, a, b);
+        else wdec16(l, h, a, b);
+    };
+    const int n = nx > ny ? ny : nx;
+    int p = 1;
+    while (p <= n) p <<= 1;
+    p >>= 1;
+    int p2 = p;
+    p >>= 1;
+    while (p >= 1) {
+        uint16_t* py = in;
+        uint16_t* const ey = in + (ptrdiff_t)oy * (ny - p2);
+        const int oy1 = oy * p, oy2 = oy * p2, ox1 = ox * p, ox2 = ox * p2;
+        uint16_t i00, i01, i10, i11;
+        for (; py <= ey; py += oy2) {
+            uint16_t* px = py;
+            uint16_t* const ex = py + (ptrdiff_t)ox * (nx - p2);
+            for (; px <= ex; px += ox2) {
+                uint16_t* p01 = px + ox1;
+                uint16_t* p10 = px + oy1;
+                uint16_t* p11 = p10 + ox1;
+                dec(*px, *p10, i00, i10);
+                dec(*p01, *p11, i01, i11);
+                dec(i00, i01, *px, *p01);
+                dec(i10, i11, *p10, *p11);
+            }
+            if (nx & p) {  // odd column
+                uint16_t* p10 = px + oy1;
+                dec(*px, *p10, i00, *p10);
+                *px = i00;
+            }
+        }
+        if (ny & p) {  // odd line
+            uint16_t* px = py;
+            uint16_t* const ex = py + (ptrdiff_t)ox * (nx - p2);
+            for (; px <= ex; px += ox2) {
+                uint16_t* p01 = px + ox1;
+                dec(*px, *p01, i00, *p01);
+                *px = i00;
+            }
+        }
+        p2 = p;
+        p >>= 1;
+    }
+}
+
+// One PIZ chunk -> `lines` scanlines of `words` (per channel: 1 for HALF, 2
+// for FLOAT / UINT) x width samples, in the file's line-then-channel layout.
+bool uncompress(const uint8_t* in, size_t n, int width, int lines, const std::vector<int>& words,
+                std::vector<uint8_t>& raw) {
+    size_t total = 0;
+    std::vector<size_t> start(words.size());
+    for (size_t c = 0; c < words.size(); ++c) {
+        start[c] = total;
+        total += (size_t)width * lines * words[c];
+    }
+    if (n < 4) return false;
+    const uint16_t lo = (uint16_t)(in[0] | in[1] << 8), hi = (uint16_t)(in[2] | in[3] << 8);
+    size_t p = 4;
+    if (hi >= kBitmapSize) return false;
+    std::vector<uint8_t> bitmap(kBitmapSize, 0);
+    if (lo <= hi) {
+        const size_t nb = (size_t)hi - lo + 1;
+        if (nb > n - p) return false;
+        std::memcpy(bitmap.data() + lo, in + p, nb);
+        p += nb;
+    }
+    // reverse range map: the k-th value present (0 always) -> k
+    std::vector<uint16_t> lut(kUshortRange, 0);
+    int k = 0;
+    for (int i = 0; i < kUshortRange; ++i)
+        if (i == 0 || (bitmap[i >> 3] & (1 << (i & 7)))) lut[k++] = (uint16_t)i;
+    const uint16_t max_value = (uint16_t)(k - 1);
+    if (n - p < 4) return false;
+    const uint32_t length = rd32(in + p);
+    p += 4;
+    if (length > n - p) return false;
+    std::vector<uint16_t> tmp(total);
+    if (!huf_uncompress(in + p, length, tmp.data(), total)) return false;
+    for (size_t c = 0; c < words.size(); ++c)
+        for (int j = 0; j < words[c]; ++j)
+            wav2_decode(tmp.data() + start[c] + j, width, words[c], lines, width * words[c], max_value);
+    for (uint16_t& v : tmp) v = lut[v];
+    raw.resize(total * 2);
+    uint8_t* o = raw.data();
+    for (int y = 0; y < lines; ++y)
+        for (size_t c = 0; c < words.size(); ++c) {
+            const uint16_t* s = tmp.data() + start[c] + (size_t)y * width * words[c];
+            for (size_t x = 0; x < (size_t)width * words[c]; ++x) {
+                *o++ = (uint8_t)(s[x] & 0xff);
+                *o++ = (uint8_t)(s[x] >> 8);
+            }
+        }
+    return true;
+}
+
+}  // namespace piz
+
+bool decode_chunk(const ExrHeader& h, const uint8_t* data, size_t size, size_t raw_size, int lines,
+                  std::vector<uint8_t>& raw) {
+    const int compression = h.compression;
     raw.resize(raw_size);
     if (compression == BMFR_EXR_NONE || size == raw_size) {  // stored uncompressed
         if (size != raw_size) return false;
         std::memcpy(raw.data(), data, size);
         return true;
+    }
+    if (compression == BMFR_EXR_PIZ) {
+        std::vector<int> words;
+        for (const Channel& c : h.channels) words.push_back(type_bytes(c.type) / 2);
+        return piz::uncompress(data, size, h.width(), lines, words, raw) && raw.size() == raw_size;
     }
     std::vector<uint8_t> t;
     if (compression == BMFR_EXR_RLE) {
@@ -323,7 +640,7 @@ int bmfr_exr_read_rgb(const char* path, int width, int height, float* rgb) {
         if (line0 < 0 || line0 >= height || size < 0 || (uint64_t)size > file.size() - off - 8)
             return fail(std::string(path) + ": bad chunk");
         const int lines = std::min(lpc, height - line0);
-        if (!decode_chunk(h.compression, file.data() + off + 8, (size_t)size, line_bytes * lines, raw))
+        if (!decode_chunk(h, file.data() + off + 8, (size_t)size, line_bytes * lines, lines, raw))
             return fail(std::string(path) + ": corrupt chunk at y=" + std::to_string(y));
         for (int l = 0; l < lines; ++l) {
             const uint8_t* line = raw.data() + line_bytes * l;

@@ -4,10 +4,10 @@
  * (bmfr.cpp:145-163, ImageInput::open + read_image(TypeDesc::FLOAT), 3
  * channels) and the PNG output of bmfr.cpp:519-553 (ImageOutput, FLOAT ->
  * 8 bit).  Self-contained over zlib: scanline OpenEXR 2.x single-part files
- * with HALF / FLOAT / UINT channels and NONE, RLE, ZIPS or ZIP compression
- * (the formats of the BMFR dataset and of common renderers; PIZ, PXR24,
- * B44 and DWA and tiled / deep / multi-part files are rejected with an
- * error); writer: FLOAT RGB, NONE or ZIP.
+ * with HALF / FLOAT / UINT channels and NONE, RLE, ZIPS, ZIP or PIZ
+ * compression (the formats of the BMFR dataset and of common renderers;
+ * PXR24, B44 and DWA and tiled / deep / multi-part files are rejected with
+ * an error); writer: FLOAT RGB, NONE or ZIP.
  */
 #ifndef BMFR_IMAGE_IO_H
 #define BMFR_IMAGE_IO_H
@@ -22,7 +22,8 @@ typedef enum bmfr_exr_compression {
     BMFR_EXR_NONE = 0,
     BMFR_EXR_RLE = 1,
     BMFR_EXR_ZIPS = 2,
-    BMFR_EXR_ZIP = 3
+    BMFR_EXR_ZIP = 3,
+    BMFR_EXR_PIZ = 4  /* read only */
 } bmfr_exr_compression;
 
 /* Size of an EXR file's data window.  0 on success, else -1 (message via

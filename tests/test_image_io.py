@@ -1,7 +1,9 @@
 """EXR / PNG I/O of the host (host/image_io.cpp), checked
 against an independent numpy + zlib implementation of the same published
 formats written here: OpenEXR 2 scanline files (HALF / FLOAT channels,
-NONE / RLE / ZIPS / ZIP compression) and 8-bit RGB PNG."""
+NONE / RLE / ZIPS / ZIP compression, and PIZ through the independent encoder
+tests/exr_piz_py.py) and 8-bit RGB PNG.  EXR parity is unpinned: no OpenEXR
+library and no reference .exr file exist here."""
 from __future__ import annotations
 
 import ctypes as C
@@ -13,6 +15,8 @@ import numpy as np
 import pytest
 
 from bmfr_amd import _build
+import exr_piz_py
+from exr_piz_py import piz_compress
 
 LIB = None
 
@@ -62,7 +66,8 @@ def _rle(data: bytes) -> bytes:
 
 
 def write_exr_py(path, img: dict, compression: int, half: bool):
-    """img: channel name -> (H, W) float array.  Channels are stored sorted by name."""
+    """img: channel name -> (H, W) float array.  Channels are stored sorted by
+    name.  compression 0 NONE, 1 RLE, 2 ZIPS, 3 ZIP, 4 PIZ."""
     names = sorted(img)
     H, W = img[names[0]].shape
     ptype, dt = (1, np.float16) if half else (2, np.float32)
@@ -74,7 +79,7 @@ def write_exr_py(path, img: dict, compression: int, half: bool):
            _attr("pixelAspectRatio", "float", struct.pack("<f", 1)) +
            _attr("screenWindowCenter", "v2f", struct.pack("<ff", 0, 0)) +
            _attr("screenWindowWidth", "float", struct.pack("<f", 1)) + b"\0")
-    lpc = {0: 1, 1: 1, 2: 1, 3: 16}[compression]
+    lpc = {0: 1, 1: 1, 2: 1, 3: 16, 4: 32}[compression]
     chunks = []
     for y0 in range(0, H, lpc):
         raw = b"".join(np.ascontiguousarray(img[n][y, :]).astype(dt).tobytes()
@@ -83,6 +88,8 @@ def write_exr_py(path, img: dict, compression: int, half: bool):
             data = _rle(_predict(raw))
         elif compression in (2, 3):
             data = zlib.compress(_predict(raw))
+        elif compression == 4:
+            data = piz_compress(raw, W, min(H, y0 + lpc) - y0, [1 if half else 2] * len(names))
         else:
             data = raw
         if len(data) >= len(raw):
@@ -180,7 +187,7 @@ def test_exr_write_read_roundtrip(tmp_path, comp):
     assert read_exr_py(path.decode()).tobytes() == img.tobytes()
 
 
-@pytest.mark.parametrize("comp", [0, 1, 2, 3])
+@pytest.mark.parametrize("comp", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("half", [False, True])
 def test_exr_reader_against_reference_encoder(tmp_path, comp, half):
     img = _img(41, 29, seed=comp + 7 * half)
@@ -216,3 +223,27 @@ def test_png_quantisation(tmp_path):
     got = read_png_py(path.decode())
     want = np.floor(np.clip(np.nan_to_num(img, nan=0.0), 0, 1) * 255 + 0.5).astype(np.uint8)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (33, 70), (7, 300), (64, 5), (40, 300)])
+@pytest.mark.parametrize("half", [False, True])
+def test_exr_piz_shapes(tmp_path, shape, half):
+    """PIZ: partial last chunks, one-pixel and very wide / narrow images (odd
+    wavelet rows / columns at every level), smooth data (14-bit wavelet,
+    long runs) and noise (16-bit wavelet: many distinct words)."""
+    H, W = shape
+    rng = np.random.default_rng(H * 1000 + W)
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    smooth = (np.sin(xx / 9.0) + yy / 50.0).astype(np.float32)
+    img = np.stack([smooth, rng.normal(0, 10, (H, W)).astype(np.float32), np.zeros((H, W), np.float32)], -1)
+    img[:, :, 2][::3] = 0.5  # runs
+    chans = {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2]}
+    path = str(tmp_path / "piz.exr")
+    exr_piz_py.MAX_VALUES.clear()
+    write_exr_py(path, chans, 4, half)
+    if shape == (40, 300) and not half:  # both wavelet forms: the first chunk 16-bit, the 8-line tail 14-bit
+        assert max(exr_piz_py.MAX_VALUES) >= 1 << 14 and min(exr_piz_py.MAX_VALUES) < 1 << 14
+    out = np.empty_like(img)
+    assert lib().bmfr_exr_read_rgb(path.encode(), W, H, out.ctypes.data) == 0, lib().bmfr_io_error()
+    want = img.astype(np.float16).astype(np.float32) if half else img
+    np.testing.assert_array_equal(out, want)
