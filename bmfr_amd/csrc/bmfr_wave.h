@@ -39,34 +39,52 @@ __device__ __forceinline__ float swap32_down(float v) {
     return __int_as_float(p[1]);
 }
 
+// Step 3 of a sum (64 -> 8, bmfr.cl:35-36) for lanes 0..7:
+// s[i] + ((((((s[i+8] + s[i+16]) + s[i+24]) + s[i+32]) + s[i+40]) + s[i+48]) + s[i+56]).
+// Rows R0..R3 = lanes 0-15 .. 48-63.  One permlane16 swap gives
+// e = (R0, R0, R2, R2) and o = (R1, R1, R3, R3) (s's even rows stay where
+// they are, so only one copy of s is made); the running sum is formed on
+// lanes 0-7 over R0's upper half and R1, moved to lanes 32-39 to take R2 and
+// R3 there, and moved back for s[i]: 7 adds (4 with a fused DPP row shift),
+// three permlane swaps, two moves.
+__device__ __forceinline__ float sum_step3(float s) {
+    const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_int(s), __float_as_int(s), false, false);
+    const float e = __int_as_float(sw[0]), o = __int_as_float(sw[1]);
+    const float lo = (dpp_shl8(e) + o) + dpp_shl8(o);  // lanes 0-7: (s[i+8] + s[i+16]) + s[i+24]
+    const int junk = __builtin_nondeterministic_value(0);
+    const float up = __int_as_float(__builtin_amdgcn_permlane32_swap(junk, __float_as_int(lo), false, false)[0]);
+    // lanes 32-39: (((lo + s[i+32]) + s[i+40]) + s[i+48]) + s[i+56]
+    const float hi = (((up + e) + dpp_shl8(e)) + o) + dpp_shl8(o);
+    // (o is dead by now: its lower half takes hi's upper half)
+    const float down =
+        __int_as_float(__builtin_amdgcn_permlane32_swap(__float_as_int(hi), __float_as_int(o), false, false)[1]);
+    return e + down;  // lanes 0-7
+}
+
 // Steps 64 -> 8 -> 1 of parallel_reduction_{sum,max,min} (bmfr.cl:35-42,
 // 55-63, 77-85) on the 64 step-2 values s (one per lane).  Wave-uniform result.
 template <RedOp OP>
 __device__ __forceinline__ float wave_tree(float s) {
-    const float a = dpp_shl8(s);       // s[l+8]
-    const float b = swap16_down(s);    // s[l+16]
-    const float c = dpp_shl8(b);       // s[l+24]
-    const float d = swap32_down(s);    // s[l+32]
-    const float e = dpp_shl8(d);       // s[l+40]
-    const float f = swap16_down(d);    // s[l+48]
-    const float h = dpp_shl8(f);       // s[l+56]
-    float x;
     if constexpr (OP == RedOp::Sum) {
-        x = s + ((((((a + b) + c) + d) + e) + f) + h);
-    } else {
-        x = red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(s, a), b), c), d), e), f), h);
-    }
-    // Step 4, ((x0 op x1) op x2) ... op x7 over lanes 0..7, as a serial DPP
-    // scan: after pass k, lane k holds the sum of x0..xk (one DPP op per pass,
-    // instead of a readlane + a scalar-operand op per term).
-    // (Sums only: a DPP-moved operand of fmaxf / fminf would first be
-    // canonicalised, one more instruction per pass.)
-    if constexpr (OP == RedOp::Sum) {
+        // Step 4, ((x0 + x1) + x2) ... + x7 over lanes 0..7, as a serial DPP
+        // scan: after pass k, lane k holds the sum of x0..xk (one DPP op per
+        // pass, instead of a readlane + a scalar-operand op per term).
+        const float x = sum_step3(s);
         float r = x;
 #pragma unroll
         for (int k = 1; k < 8; ++k) r = dpp_shr1(r) + x;
         return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 7));
     } else {
+        // (min / max: a DPP-moved operand of fmaxf / fminf is first
+        // canonicalised, so the plain form is as short)
+        const float a = dpp_shl8(s);       // s[l+8]
+        const float b = swap16_down(s);    // s[l+16]
+        const float c = dpp_shl8(b);       // s[l+24]
+        const float d = swap32_down(s);    // s[l+32]
+        const float e = dpp_shl8(d);       // s[l+40]
+        const float f = swap16_down(d);    // s[l+48]
+        const float h = dpp_shl8(f);       // s[l+56]
+        const float x = red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(red<OP>(s, a), b), c), d), e), f), h);
         float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
 #pragma unroll
         for (int k = 1; k < 8; ++k) r = red<OP>(r, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), k)));
