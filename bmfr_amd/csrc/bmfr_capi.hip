@@ -46,6 +46,10 @@ struct bmfr_ctx {
     unsigned* reach_dev = nullptr;
     volatile unsigned* reach_host = nullptr;
     hipEvent_t reach_event = nullptr;  // after the last frame's K2
+    // One-launch frames (untiled canonical half-tmp_data path): per K1 block
+    // the epoch of the last launch that completed it; epoch counts launches.
+    unsigned* done = nullptr;
+    unsigned epoch = 0;
     // Profiling ring: 3 events per frame (before K1, after K1, after K2).
     int prof_capacity = 0;
     int prof_stride = 1;  // record frames whose number is a multiple of this
@@ -123,6 +127,8 @@ bmfr_status validate(const bmfr_config* c) {
 }
 
 bool is_tiled(const bmfr_config* c) { return c->tile_width > 0; }
+// One completion flag per block of the (untiled) frame's block grid.
+size_t done_bytes(const bmfr_ctx* c) { return (size_t)c->P.blocks_x * c->P.blocks_y * sizeof(unsigned); }
 // The stage kernels take the reference's whole-frame f32 layouts only.
 bool stage_api_ok(const bmfr_config* c) { return !is_tiled(c) && !c->input_half; }
 
@@ -328,6 +334,10 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
             e = hipEventCreateWithFlags(&c->reach_event, hipEventDisableTiming);
         }
     }
+    if (e == hipSuccess && bmfr::frame_fused_supported(c->P)) {
+        e = hipMalloc(&c->done, done_bytes(c));
+        if (e == hipSuccess) e = hipMemset(c->done, 0, done_bytes(c));
+    }
     if (e != hipSuccess) {
         bmfr_destroy(c);
         return hip_status(e);
@@ -340,6 +350,7 @@ bmfr_status bmfr_destroy(bmfr_ctx* c) {
     if (!c) return BMFR_ERROR_INVALID_ARGUMENT;
     DeviceGuard guard(c->device);
     (void)hipFree(c->reach_dev);
+    (void)hipFree(c->done);
     if (c->reach_host) (void)hipHostFree(const_cast<unsigned*>(c->reach_host));
     if (c->reach_event) (void)hipEventDestroy(c->reach_event);
     for (int i = 0; i < 2; ++i) {
@@ -491,6 +502,8 @@ bmfr::FusedArgs frame_args(const bmfr_ctx* c, const bmfr_frame_inputs* in, const
     A.reach = c->reach_dev;
     A.reach_host = const_cast<unsigned*>(c->reach_host);
     A.stamps = c->stamps;
+    A.done = nullptr;  // set per launch (one_launch_args)
+    A.epoch = 0;
     return A;
 }
 
@@ -600,6 +613,15 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
     if (part == 2) {
         if (bmfr::fused_supported(P) && (st = hip_status(noise_for_frame(c, P, s, frame_number, &A.noise_table))))
             return st;
+        if (c->done && !ev) {  // one launch: the next epoch (never 0; flags reset on wrap)
+            if (++c->epoch == 0) {
+                if ((st = hip_status(hipMemsetAsync(c->done, 0, done_bytes(c), s))))
+                    return st;
+                c->epoch = 1;
+            }
+            A.done = c->done;
+            A.epoch = c->epoch;
+        }
         st = hip_status(bmfr::launch_fused_frame(P, s, A, ev ? ev[1] : nullptr));
         if (st != BMFR_OK) return st;
     } else {

@@ -30,6 +30,34 @@ struct __attribute__((packed, aligned(4))) f3mem {
     float x, y, z;
 };
 
+// Device-coherent plane accesses, for data one work-group of a launch hands
+// to another that may run on another XCD (each XCD's L2 is write-back and
+// not coherent with the others'): raw buffer loads / stores with the sc1
+// cache policy, which the memory model uses for agent-scope atomics --
+// coherent at device scope without flushing or invalidating any L2.
+typedef __amdgpu_buffer_rsrc_t CohPlane;
+__device__ __forceinline__ CohPlane coh_plane(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, -1, 0x00020000);
+}
+constexpr int kSc1 = 16;  // buffer instruction cache-policy bit SC1
+__device__ __forceinline__ f3 ld3_coh(CohPlane r, uint32_t i) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, i * 12u, 0, kSc1);
+    return f3{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2])};
+}
+__device__ __forceinline__ void st3_coh(CohPlane r, uint32_t i, f3 v) {
+    typedef unsigned u3 __attribute__((ext_vector_type(3)));
+    __builtin_amdgcn_raw_buffer_store_b96(u3{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z)}, r,
+                                          i * 12u, 0, kSc1);
+}
+__device__ __forceinline__ float2 ld2_coh(CohPlane r, uint32_t i) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, i * 8u, 0, kSc1);
+    return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+}
+__device__ __forceinline__ void st2_coh(CohPlane r, uint32_t i, float2 v) {
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(u2{__float_as_uint(v.x), __float_as_uint(v.y)}, r, i * 8u, 0, kSc1);
+}
+
 // Plane elements by pixel index i.  The address is the plane's base (a kernel
 // argument: uniform, in SGPRs) plus a 32-bit byte offset (one VGPR) -- the
 // SGPR-base form of the global memory instructions -- so the planes read at

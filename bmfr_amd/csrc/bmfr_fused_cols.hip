@@ -501,7 +501,10 @@ __device__ __forceinline__ void back_substitute_regs(Lds<B>& L, int t) {
 constexpr int kColsWaves = 4;  // minimum waves per SIMD for the register allocator (128 VGPRs: 4 WGs/CU)
 
 // One K1 work-group (block g of the launch), on the LDS area L.
-template <int NS, int FS, class IN>
+// COH: the TAA tiles of the same frame run in this launch: the accumulated
+// colour and the reprojected positions they read are stored device-coherent
+// and the block publishes done[g] = epoch once they are.
+template <int NS, int FS, class IN, bool COH = false>
 __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, Lds<NS + FS + 3>& L, int g) {
     constexpr int B = NS + FS + 3;
     const int t = threadIdx.x;
@@ -557,7 +560,8 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
             if (it.owner) {
                 st3(A.noisy_out, it.lin, it.color);
                 st_px(A.spp_out, it.lin, it.spp);
-                st_px(A.prev_pixel_out, it.lin, make_float2(it.pfx, it.pfy));
+                if constexpr (COH) st2_coh(coh_plane(A.prev_pixel_out), it.lin, make_float2(it.pfx, it.pfy));
+                else st_px(A.prev_pixel_out, it.lin, make_float2(it.pfx, it.pfy));
             }
             if (i & 1) {  // rows j = 4w + i - 1, 4w + i: adjacent halves of lane l's row slot
                 // (pair 2w + i/2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)
@@ -648,7 +652,8 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
             const int t3 = l3 + 64 * w;
             const f3 prev{L.keep[i][0][t3], L.keep[i][1][t3], L.keep[i][2][t3]};
             const f3 acc{alpha * ci.x + beta * prev.x, alpha * ci.y + beta * prev.y, alpha * ci.z + beta * prev.z};
-            st3(A.acc_out, lin[i], acc);
+            if constexpr (COH) st3_coh(coh_plane(A.acc_out), lin[i], acc);
+            else st3(A.acc_out, lin[i], acc);
         }
     }
 #ifdef BMFR_STAMPS
@@ -656,6 +661,11 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 #endif
     BMFR_STAMP(5);
 #undef BMFR_STAMP
+    if constexpr (COH) {
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's stores are performed
+        lds_barrier();                       // ... and every wave's
+        if (t == 0) __hip_atomic_store(&A.done[g], A.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // First round of work-groups: start the k-th group of 256 k * kStagger
@@ -676,14 +686,21 @@ __global__ __launch_bounds__(kThreads, kColsWaves) void k_fused_cols(Params P, K
     k1_cols_body<NS, FS, IN>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
 }
 
-// K1 of frame f and K2 (64 x kSeqTaaH tiles) of frame f - 1 in one launch:
-// work-groups [0, nk1) are K1 blocks, [nk1p, nk1p + nk2) TAA tiles (nk1p = nk1
-// rounded up to the 8 XCDs; the ones between exit).  The in-order dispatch
-// runs the tiles in K1's tail, where its last work-groups leave CUs idle, and
-// a frame costs one launch.  K2 of f - 1 reads frame f - 1's state, which K1
-// of f does not write (double-buffered), and frame f - 2's TAA output.
+// K1 and K2 (64 x kSeqTaaH tiles) in one launch: work-groups [0, nk1) are K1
+// blocks, [nk1p, nk1p + nk2) TAA tiles (nk1p = nk1 rounded up to the 8 XCDs;
+// the ones between exit).  The in-order dispatch runs the tiles in K1's
+// tail, where its last work-groups leave CUs idle, and a frame costs one
+// launch.
+//   SAME = false (bmfr_process_sequence): K1 of frame f with K2 of frame
+//     f - 1, which reads frame f - 1's state (K1 of f does not write it:
+//     double-buffered) and frame f - 2's TAA output.
+//   SAME = true (bmfr_process_frame): K1 and K2 of one frame; a tile waits
+//     for the K1 blocks under its footprint (completion flags) and reads
+//     their outputs device-coherent.  Work-groups of one XCD are dispatched
+//     in order, so every K1 block a waiting tile needs has been dispatched:
+//     the waits end.
 constexpr int kSeqTaaH = 12;
-template <int NS, int FS, class IN>
+template <int NS, int FS, class IN, bool SAME = false>
 __global__ __launch_bounds__(kThreads, 4) void k_fused_cols_taa(Params P, K1Args A, Params P2, TaaArgs T, int nk1,
                                                                 int nk1p) {
     constexpr int HW = 64 + 2, N = HW * (kSeqTaaH + 2);
@@ -698,12 +715,12 @@ __global__ __launch_bounds__(kThreads, 4) void k_fused_cols_taa(Params P, K1Args
     const int b = blockIdx.x;
     if (b < nk1) {
         k1_stagger(b, nk1);
-        k1_cols_body<NS, FS, IN>(P, A, U.k1, xcd_swizzle(b, nk1));
+        k1_cols_body<NS, FS, IN, SAME>(P, A, U.k1, xcd_swizzle(b, nk1));
     } else if (b >= nk1p) {
         const int gx = (P2.tx1 - P2.tx0 + 63) / 64, n2 = (int)gridDim.x - nk1p;
         const int gi = xcd_swizzle(b - nk1p, n2);
-        taa_tile<IN, kSeqTaaH>(P2, T, P2.tx0 + (gi % gx) * 64, P2.ty0 + (gi / gx) * kSeqTaaH, U.k2.Y, U.k2.sE,
-                               U.k2.sRP);
+        taa_tile<IN, kSeqTaaH, SAME>(P2, T, P2.tx0 + (gi % gx) * 64, P2.ty0 + (gi / gx) * kSeqTaaH, U.k2.Y,
+                                     U.k2.sE, U.k2.sRP);
     }
 }
 
@@ -718,6 +735,22 @@ static void launch_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
 }
 
 bool seq_fused_supported(const Params& P) { return fused_cols_supported(P) && P.ring == 0; }
+// (untiled: a tiled context's K2 also forwards the reach report, k_fused_taa)
+bool frame_fused_supported(const Params& P) { return seq_fused_supported(P) && !P.check_reach; }
+
+template <int FS, class IN>
+static void launch_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
+    const int nk1 = k1_blocks(P), nk1p = (nk1 + 7) & ~7;
+    const int nk2 = ((P.tx1 - P.tx0 + 63) / 64) * ((P.ty1 - P.ty0 + cols::kSeqTaaH - 1) / cols::kSeqTaaH);
+    hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN, true>), dim3(nk1p + nk2), dim3(cols::kThreads), 0, st, P,
+                       k1_args(A), P, taa_args(A), nk1, nk1p);
+}
+
+hipError_t launch_fused_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
+    if (P.scaled == 6) P.input_half ? launch_frame_one<6, _Float16>(P, st, A) : launch_frame_one<6, float>(P, st, A);
+    else P.input_half ? launch_frame_one<9, _Float16>(P, st, A) : launch_frame_one<9, float>(P, st, A);
+    return hipGetLastError();
+}
 
 template <int FS, class IN>
 static void launch_cols_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,

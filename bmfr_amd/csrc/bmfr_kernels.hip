@@ -275,6 +275,8 @@ hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A) 
 
 hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& A, hipEvent_t mid) {
     hipError_t e;
+    // One launch for the frame, unless K1 and K2 are timed apart (mid event).
+    if (!mid && A.done && frame_fused_supported(P)) return launch_fused_frame_one(P, st, A);
     if (fused_supported(P)) {
         if ((e = launch_fused_k1_blocks(P, st, A)) != hipSuccess) return e;
         if (mid) (void)hipEventRecord(mid, st);

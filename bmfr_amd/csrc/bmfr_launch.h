@@ -40,6 +40,8 @@ struct FusedArgs {
     unsigned* reach;      // tiled contexts: max overshoot (px) of reprojection taps past the valid state
     unsigned* reach_host; // tiled contexts: page-locked report of it (see TaaArgs)
     unsigned long long* stamps;  // diagnostic build: 8 timestamps per block, or null
+    unsigned* done;       // one-launch frame: per K1 block, the epoch of the launch that completed it
+    unsigned epoch;       // this launch's epoch (context-wide launch counter, never 0)
 };
 
 // Kernel arguments of the fused K1 (canonical feature lists).
@@ -55,14 +57,16 @@ struct K1Args {
     const double* noise;
     unsigned* reach;
     unsigned long long* stamps;
+    unsigned* done;
+    unsigned epoch;
 };
 inline K1Args k1_args(const FusedArgs& A) {
-    return K1Args{A.in,      A.cam,          A.frame,          A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out,
-                  A.acc_out, A.noise_table,  A.reach,          A.stamps};
+    return K1Args{A.in,      A.cam,         A.frame, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out,
+                  A.acc_out, A.noise_table, A.reach, A.stamps,   A.done,      A.epoch};
 }
 inline TaaArgs taa_args(const FusedArgs& A) {
     return TaaArgs{A.acc_out, A.albedo, A.prev_pixel_out, A.result_out, A.result_prev, A.frame, A.reach,
-                   A.reach_host};
+                   A.reach_host, A.done, A.epoch};
 }
 
 bool fitter_supported(int not_scaled, int scaled);
@@ -100,6 +104,11 @@ hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedAr
 // Sequence kernel (bmfr_process_sequence): K1 of a frame (A, or none) and K2
 // of the frame before it (A2, or none) in one launch.
 bool seq_fused_supported(const Params& P);
+// One-launch frame (bmfr_process_frame, untiled): K1 blocks, then the TAA
+// tiles of the same frame, each waiting on the completion flags of the K1
+// blocks under its footprint.
+bool frame_fused_supported(const Params& P);
+hipError_t launch_fused_frame_one(const Params& P, hipStream_t st, const FusedArgs& A);
 hipError_t launch_fused_k1_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
                                const FusedArgs* A2);
 hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A);

@@ -24,7 +24,33 @@ struct TaaArgs {
     // cleared for the next frame.
     unsigned* reach_dev;
     unsigned* reach_host;
+    // One-launch frame (COH tiles): K1 block g of this launch has stored its
+    // accumulated colour and reprojected positions once done[g] >= epoch.
+    const unsigned* done;
+    unsigned epoch;
 };
+
+// A COH tile first waits until every K1 block owning a pixel of the tile or
+// its 1-px halo (the blocks of the frame's shifted grid, bmfr.cl:267-285)
+// has published: at most 4 x 2 blocks, one lane each, bounded polls (a
+// protocol error would give wrong pixels, not a wave that never ends).
+__device__ __forceinline__ void wait_k1_blocks(const Params& P, const TaaArgs& T, int x0, int y0, int th) {
+    const int2 off = kBlockOffsets[T.frame & 15];
+    const int xa = max(x0 - 1, P.ox), xb = min(x0 + 64, P.ox + P.stride - 1);
+    const int ya = max(y0 - 1, P.oy), yb = min(y0 + th, P.oy + P.rows - 1);
+    const int bxa = (xa + kEdge / 2 - off.x) / kEdge, bxb = (xb + kEdge / 2 - off.x) / kEdge;
+    const int bya = (ya + kEdge / 2 - off.y) / kEdge, byb = (yb + kEdge / 2 - off.y) / kEdge;
+    const int nx = bxb - bxa + 1, n = nx * (byb - bya + 1);
+    const int t = threadIdx.x;
+    if (t < n) {
+        const int bx = bxa + t % nx, by = bya + t / nx;
+        const unsigned* f = T.done + (by - P.by0) * P.nbx + (bx - P.bx0);
+        for (int k = 0; k < (1 << 22) && __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < T.epoch;
+             ++k)
+            __builtin_amdgcn_s_sleep(2);
+    }
+    __syncthreads();
+}
 
 __device__ __forceinline__ void forward_reach(const TaaArgs& T) {
     if (T.reach_dev && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
@@ -38,7 +64,9 @@ __device__ __forceinline__ void forward_reach(const TaaArgs& T) {
 }
 
 // Y: (64 + 2) * (TH + 2) float4; sE / sRP: the powr tables' LDS copies.
-template <class IN, int TH>
+// COH: the tile runs in the launch that computes its K1 blocks: it waits for
+// them and reads their outputs with device-coherent loads.
+template <class IN, int TH, bool COH = false>
 __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int x0, int y0, float4* __restrict__ Y,
                                          double* __restrict__ sE, double2* __restrict__ sRP) {
     static_assert(TH % 4 == 0 && TH >= 4, "tile height");
@@ -49,11 +77,16 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
     const int t = threadIdx.x;
     bmfr_powr_tables_to_lds<256>(sE, sRP, t);
     const int tx = t & (64 - 1), ty = t >> 6;
+    if constexpr (COH) wait_k1_blocks(P, T, x0, y0, TH);
+    const CohPlane c_pp = coh_plane(T.prev_pixel), c_src = coh_plane(T.src);  // (unused unless COH)
     // Reprojected positions first, then the tile and its ring behind them.
     float2 pf[KN];
 #pragma unroll
-    for (int k = 0; k < KN; ++k)
-        pf[k] = ld_px(T.prev_pixel, pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + ty + 4 * k, P.ty1 - 1)));
+    for (int k = 0; k < KN; ++k) {
+        const uint32_t i = pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + ty + 4 * k, P.ty1 - 1));
+        if constexpr (COH) pf[k] = ld2_coh(c_pp, i);
+        else pf[k] = ld_px(T.prev_pixel, i);
+    }
     f3 v[KN + 1], al[KN + 1];
     int hx = 0, hy = 0;  // this thread's ring pixel (t < RING), in tile + halo coordinates
     if (t < 2 * HW) {
@@ -71,7 +104,8 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
         // whose last 64-px column or TH-row band overhangs its output reads
         // no pixel outside the region; such values reach no output pixel.
         const uint32_t lin = pix(P, clamp_rx(P, x0 - 1 + lx), clamp_ry(P, y0 - 1 + ly));
-        v[k] = ld3(T.src, lin);
+        if constexpr (COH) v[k] = ld3_coh(c_src, lin);
+        else v[k] = ld3(T.src, lin);
         al[k] = ld3in<IN>(T.albedo, lin);
     }
     // Previous-frame taps before the tone map: their latency hides under it.
