@@ -2,7 +2,10 @@
 """Cost of the tiled frame path on one GPU, without the exchange: rank r's
 tile of a tx x ty grid of W x H tiles, each frame as process_frame or as
 process_frame_interior + process_frame_border (halo left stale: timing only),
-against the untiled W x H frame.  Prints ms/frame for each."""
+against the untiled W x H frame.  Prints ms/frame for each.
+
+  python tools/tile_cost.py [W H TX TY RANK]   (default: 3840 2160 4 2 5;
+  the 8K strong-scaling tile of 8 GPUs: 1920 2160 4 2 5)"""
 import os
 import sys
 import time
@@ -13,7 +16,8 @@ import torch  # noqa: E402
 import bmfr_amd  # noqa: E402
 from bmfr_amd import tiling  # noqa: E402
 
-W, H, TX, TY, RANK, FR = 3840, 2160, 4, 2, 5, 30
+W, H, TX, TY, RANK = (int(x) for x in (sys.argv[1:6] if len(sys.argv) > 5 else (3840, 2160, 4, 2, 5)))
+FR = 30
 grid = tiling.TileGrid(W * TX, H * TY, TX, TY, halo=64)
 
 
