@@ -2,7 +2,7 @@
 # and PMC passes (one counter group per run, each under its own time limit).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/prof_r02b
+O=gpurun_out/prof_r02c
 mkdir -p $O
 P="python3 tools/k1_frames.py 3840 2160 12"
 step() { local name=$1; shift; timeout -s KILL 150 "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; return $rc; }
