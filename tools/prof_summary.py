@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output for profiles/.
 
-  prof_summary.py stats <dir>          kernel_stats.csv -> markdown table
+  prof_summary.py stats <dir>          kernel_stats.csv -> markdown table, then per (kernel, grid)
   prof_summary.py pmc <dir> <counter>  counter_collection.csv -> per-kernel mean
   prof_summary.py calib <dir> <counter> <bytes>   counter / true bytes per calibration kernel
   prof_summary.py traffic <fetch_dir> <write_dir> <workload> <pixels> <alg_bytes_per_px>
@@ -55,6 +55,22 @@ def stats(d):
     return "\n".join(out)
 
 
+def by_grid(d):
+    """Per (kernel, grid size): dispatches and mean / median duration from the
+    kernel trace -- separates the image sizes one bench command runs."""
+    rows = list(csv.DictReader(open(find(d, "*kernel_trace.csv"))))
+    per = {}
+    for r in rows:
+        if not any(k in r["Kernel_Name"] for k in ("bmfr", "k_synth")):
+            continue
+        key = (short(r["Kernel_Name"]), int(r["Grid_Size_X"]) // max(int(r["Workgroup_Size_X"]), 1))
+        per.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    out = ["| kernel | work-groups | dispatches | mean us | median us |", "|---|---|---|---|---|"]
+    for (k, g), v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+        out.append(f"| {k} | {g} | {len(v)} | {statistics.mean(v):.1f} | {statistics.median(v):.1f} |")
+    return "\n".join(out)
+
+
 def pmc(d, counter):
     rows = list(csv.DictReader(open(find(d, "*counter_collection.csv"))))
     per = {}
@@ -99,6 +115,10 @@ def main():
     cmd = sys.argv[1]
     if cmd == "stats":
         print(stats(sys.argv[2]))
+        print()
+        print("Per work-group count (one bench command runs several image sizes):")
+        print()
+        print(by_grid(sys.argv[2]))
     elif cmd == "pmc":
         print(json.dumps(pmc(sys.argv[2], sys.argv[3]), indent=1))
     elif cmd == "calib":
