@@ -110,7 +110,8 @@ def parse():
     ap.add_argument("--no-8k", action="store_true", help="skip the untiled 7680x4320 line (N = 1) / the 1-GPU "
                                                          "reference time (N > 1)")
     ap.add_argument("--frames-8k", type=int, default=30, help="timed frames of the untiled 8K line (N = 1)")
-    ap.add_argument("--cpu-frames", type=int, default=2, help="timed CPU-oracle frames (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=12,
+                    help="timed CPU-oracle frames (0 = skip); 12 at 4K is ~10 s of host work")
     ap.add_argument("--seed", type=int, default=0x424D4652)
     ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
                     help="multi-GPU: strong = one --width x --height frame split (default), "
