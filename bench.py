@@ -140,7 +140,9 @@ def cpu_baseline(cfg: bmfr_amd.BmfrConfig, frames: int, seed: int):
                                                  cfg.use_half_precision_in_tmp_data))
     times = []
     for f in range(frames + 1):
-        fr = bmfr_amd.synth_frame_host(W, H, f, seed=seed)
+        # the frame the GPU runs process (the GPU renderer), copied to host memory
+        g = bmfr_amd.synth_frame_device(W, H, f, seed=seed)
+        fr = {k: g[k].cpu().numpy().reshape(H, W, 3) for k in ("noisy", "normals", "positions", "albedo")}
         vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
         _, jit = bmfr_amd.synth_camera(W, H, f)
         loop.upload(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"])
