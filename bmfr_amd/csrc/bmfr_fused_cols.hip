@@ -518,6 +518,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 #define BMFR_STAMP(k) (void)0
 #endif
     BMFR_STAMP(0);
+#ifdef BMFR_STAMPS
+    if (t == 0 && A.stamps) A.stamps[(size_t)g * 8 + 6] = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+#endif
     int bx, by;
     k1_block(P, g, bx, by);
     const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
@@ -660,6 +663,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     __syncthreads();
 #endif
     BMFR_STAMP(5);
+#ifdef BMFR_STAMPS
+    if (t == 0 && A.stamps) A.stamps[(size_t)g * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+#endif
 #undef BMFR_STAMP
     if constexpr (COH) {
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's stores are performed

@@ -21,25 +21,31 @@ import torch  # noqa: E402
 import bmfr_amd  # noqa: E402
 
 W, H = (int(x) for x in (sys.argv[1:3] if len(sys.argv) > 2 else (3840, 2160)))
+# frames whose K1 phases to report (the stamps hold the last frame's blocks)
+report = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [3]
 cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H)
 den = bmfr_amd.Denoiser(cfg)
-frames = [bmfr_amd.synth_frame_device(W, H, f) for f in range(4)]
-for f in range(4):
+G = den.sizes.blocks
+names = ["accumulate_noisy", "min/max scale", "QR", "back-subst", "weighted+blend"]
+for f in range(max(report) + 1):
+    fr = bmfr_amd.synth_frame_device(W, H, f)
     vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
     _, jit = bmfr_amd.synth_camera(W, H, f)
-    fr = frames[f]
     den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, f)
-torch.cuda.synchronize()
-G = den.sizes.blocks
-buf = np.zeros(G * 8, np.uint64)
-rc = den.lib.bmfr_debug_stamps(den.handle, buf.ctypes.data_as(C.c_void_p), buf.size)
-assert rc == 0, rc
-st = buf.reshape(G, 8).astype(np.int64)
-names = ["accumulate_noisy", "min/max scale", "QR", "back-subst", "weighted+blend"]
-d = np.diff(st[:, :6], axis=1)
-tot = st[:, 5] - st[:, 0]
-print(f"{W}x{H}: {G} blocks; block lifetime cycles median {np.median(tot):.0f} mean {tot.mean():.0f}")
-for i, n in enumerate(names):
-    print(f"  {n:18s} median {np.median(d[:, i]):8.0f}  mean {d[:, i].mean():8.0f}  share {d[:, i].sum() / tot.sum():.2%}")
-span = st[:, 5].max() - st[:, 0].min()
-print(f"  kernel span (cycles) {span}, start spread {st[:, 0].max() - st[:, 0].min()}")
+    if f not in report:
+        continue
+    torch.cuda.synchronize()
+    buf = np.zeros(G * 8, np.uint64)
+    rc = den.lib.bmfr_debug_stamps(den.handle, buf.ctypes.data_as(C.c_void_p), buf.size)
+    assert rc == 0, rc
+    st = buf.reshape(G, 8).astype(np.int64)
+    d = np.diff(st[:, :6], axis=1)
+    tot = st[:, 5] - st[:, 0]
+    print(f"{W}x{H} frame {f}: {G} blocks; block lifetime cycles median {np.median(tot):.0f} mean {tot.mean():.0f}")
+    for i, n in enumerate(names):
+        print(f"  {n:18s} median {np.median(d[:, i]):8.0f}  mean {d[:, i].mean():8.0f}  share {d[:, i].sum() / tot.sum():.2%}")
+    rt = st[:, 7] - st[:, 6]
+    ok = rt > 0
+    print(f"  shader clock (block cycles / 100 MHz realtime) median {np.median(tot[ok] / rt[ok]) * 0.1:.3f} GHz")
+    span = st[:, 5].max() - st[:, 0].min()
+    print(f"  kernel span (cycles) {span}, start spread {st[:, 0].max() - st[:, 0].min()}", flush=True)
