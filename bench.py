@@ -222,7 +222,7 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         if transport is None or f == 0:
             den.process_frame(*args, **kw)
         elif not a.overlap:
-            transport.exchange_ctx(den)
+            transport.exchange_ctx(den, f)
             den.process_frame(*args, **kw)
         else:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if mark else None
@@ -235,14 +235,14 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
             with torch.cuda.stream(comm):  # one pack and one unpack kernel around the RCCL batch
                 if ev:
                     ev[2].record(comm)
-                transport.exchange_ctx(den)
+                transport.exchange_ctx(den, f)
                 if ev:
                     ev[3].record(comm)
             compute.wait_stream(comm)
             den.process_frame_border(*args, **kw)
             if ev:
                 ev[4].record(compute)
-                marks.append(ev)
+                marks.append((ev, transport.last_bytes))
         if frame_done is not None:
             frame_done.record(compute)
 
@@ -321,10 +321,12 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     noisy_tm = torch.clamp(torch.clamp(last["albedo"].float() * last["noisy"].float(), min=0) ** 0.454545, 0, 1)
     split = None
     if marks:
-        mean = lambda i, j: float(np.mean([e[i].elapsed_time(e[j]) for e in marks]))  # noqa: E731
+        mean = lambda i, j: float(np.mean([e[i].elapsed_time(e[j]) for e, _ in marks]))  # noqa: E731
+        # halo bytes per frame (the exchanged rectangles change with frame % 16)
         split = {"interior_ms": mean(0, 1), "exchange_ms": mean(2, 3), "border_ms": mean(1, 4),
                  "frame_ms": mean(0, 4),
-                 "halo_bytes_sent": int(sum(transport._layout[1])), "halo_bytes_received": int(sum(transport._layout[3])),
+                 "halo_bytes_sent": int(np.mean([b[0] for _, b in marks])),
+                 "halo_bytes_received": int(np.mean([b[1] for _, b in marks])),
                  "halo_overshoot_px": overshoot}
     res = {
         "cfg": cfg,

@@ -103,6 +103,7 @@ SIGNATURES = {
     "bmfr_process_frame": (_I, [_P, _P, C.POINTER(FrameInputs), _F16, _F2, _I]),
     "bmfr_process_frame_interior": (_I, [_P, _P, C.POINTER(FrameInputs), _F16, _F2, _I]),
     "bmfr_halo_copy": (_I, [_P, _P, C.POINTER(C.c_int), _I, _P, _I, C.POINTER(C.c_size_t)]),
+    "bmfr_halo_need": (_I, [C.POINTER(Config), _I, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "bmfr_process_sequence": (_I, [_P, _P, _I, C.POINTER(FrameInputs), _F16, _F2, _I, C.POINTER(_P)]),
     "bmfr_process_frame_border": (_I, [_P, _P, C.POINTER(FrameInputs), _F16, _F2, _I]),
     "bmfr_output": (_P, [_P]),

@@ -172,17 +172,20 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     P.vy0 = P.oy;
     P.vx1 = P.ox + P.stride;
     P.vy1 = P.oy + P.rows;
+    P.wx0 = P.vx0, P.wy0 = P.vy0, P.wx1 = P.vx1, P.wy1 = P.vy1;
     return P;
 }
 
 // The launch parameters of frame `frame` for a tiled context: the blocks of
 // that frame's shifted grid (bmfr.cl:267-285, 310-317) that cover the tile
 // plus one pixel (TAA's 3x3), and the tile as K2's output.  Blocks without a
-// pixel inside the frame own nothing and are skipped.
-Params frame_params(const bmfr_ctx* c, int frame) {
-    Params P = c->P;
-    if (!is_tiled(&c->cfg)) return P;
-    const bmfr_config& g = c->cfg;
+// pixel inside the frame own nothing and are skipped.  The previous state the
+// frame reads (bmfr_halo_need): the state planes over the pixels of those
+// blocks (mirrored at the frame border) grown by the reprojection reach --
+// tile_halo - 34 pixels of motion and one for the bilinear taps -- and the
+// TAA output over the tile grown by the same reach; both clipped to the
+// region.  [v*] / [w*] are these rectangles (K1 checks the taps against them).
+Params frame_params_cfg(const bmfr_config& g, Params P, int frame) {
     const int E = BMFR_BLOCK_EDGE_LENGTH;
     const int ox = bmfr::kBlockOffsetTable[frame & 15][0], oy = bmfr::kBlockOffsetTable[frame & 15][1];
     auto range = [&](int lo, int hi, int off, int nblocks, int& b0, int& nb) {
@@ -205,7 +208,27 @@ Params frame_params(const bmfr_ctx* c, int frame) {
     P.ty0 = g.tile_y;
     P.tx1 = g.tile_x + g.tile_width;
     P.ty1 = g.tile_y + g.tile_height;
+    const int reach = g.tile_halo - 33;
+    // [lo, hi] of the mirrored pixels of blocks [b0, b0 + nb), grown by reach, clipped to [r0, r1)
+    auto need = [&](int b0, int nb, int off, int size, int r0, int r1, int& v0, int& v1) {
+        int lo = size, hi = -1;
+        for (int p = E * b0 - E / 2 + off; p < E * (b0 + nb) - E / 2 + off; ++p) {
+            const int m = p < 0 ? -p - 1 : (p >= size ? 2 * size - p - 1 : p);
+            lo = std::min(lo, m);
+            hi = std::max(hi, m);
+        }
+        v0 = std::max(lo - reach, r0);
+        v1 = std::min(hi + 1 + reach, r1);
+    };
+    need(P.bx0, P.nbx, ox, g.image_width, P.ox, P.ox + P.stride, P.vx0, P.vx1);
+    need(P.by0, P.nby, oy, g.image_height, P.oy, P.oy + P.rows, P.vy0, P.vy1);
+    P.wx0 = std::max(P.tx0 - reach, P.ox), P.wx1 = std::min(P.tx1 + reach, P.ox + P.stride);
+    P.wy0 = std::max(P.ty0 - reach, P.oy), P.wy1 = std::min(P.ty1 + reach, P.oy + P.rows);
     return P;
+}
+
+Params frame_params(const bmfr_ctx* c, int frame) {
+    return is_tiled(&c->cfg) ? frame_params_cfg(c->cfg, c->P, frame) : c->P;
 }
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -634,6 +657,7 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
             Params I = block_rect(P, ix0, ix1, iy0, iy1);
             const bmfr_config& g = c->cfg;
             I.vx0 = g.tile_x, I.vy0 = g.tile_y, I.vx1 = g.tile_x + g.tile_width, I.vy1 = g.tile_y + g.tile_height;
+            I.wx0 = I.vx0, I.wy0 = I.vy0, I.wx1 = I.vx1, I.wy1 = I.vy1;
             st = hip_status(bmfr::launch_fused_k1_blocks(I, s, A));
             if (st != BMFR_OK) return st;
             c->pending_frame = frame_number;
@@ -807,7 +831,7 @@ bmfr_status bmfr_process_frame_border(bmfr_ctx* c, void* stream, const bmfr_fram
 
 bmfr_status bmfr_halo_copy(bmfr_ctx* c, void* stream, const int* rects, int n, void* buffer, int unpack,
                            size_t* bytes) {
-    if (!c || n < 0 || (n > 0 && !rects) || n * 4 > bmfr::kMaxHaloSegs) return BMFR_ERROR_INVALID_ARGUMENT;
+    if (!c || n < 0 || (n > 0 && !rects)) return BMFR_ERROR_INVALID_ARGUMENT;
     if (!is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;
     DeviceGuard guard(c->device);
     const int i = c->cur;  // bmfr_state(previous = 0): the last frame's state
@@ -820,11 +844,15 @@ bmfr_status bmfr_halo_copy(bmfr_ctx* c, void* stream, const int* rects, int n, v
     bmfr::HaloArgs a{};
     long long off = 0;
     for (int r = 0; r < n; ++r) {
-        const int x = rects[4 * r], y = rects[4 * r + 1], w = rects[4 * r + 2], h = rects[4 * r + 3];
+        const int* q = rects + 5 * r;
+        const int x = q[0], y = q[1], w = q[2], h = q[3], mask = q[4];
         if (w <= 0 || h <= 0 || x < s.region_x || y < s.region_y || x + w > s.region_x + s.region_width ||
-            y + h > s.region_y + s.region_height)
+            y + h > s.region_y + s.region_height || mask <= 0 || mask > BMFR_HALO_ALL)
             return BMFR_ERROR_INVALID_ARGUMENT;
-        for (const auto& p : planes) {
+        for (int k = 0; k < 4; ++k) {
+            if (!(mask & (1 << k))) continue;
+            if (a.nseg == bmfr::kMaxHaloSegs) return BMFR_ERROR_INVALID_ARGUMENT;
+            const auto& p = planes[k];
             bmfr::HaloSeg& g = a.seg[a.nseg++];
             const size_t first = ((size_t)(y - s.region_y) * s.region_width + (x - s.region_x)) * p.bpp;
             g.plane = reinterpret_cast<unsigned long long>(p.base + first);
@@ -838,6 +866,18 @@ bmfr_status bmfr_halo_copy(bmfr_ctx* c, void* stream, const int* rects, int n, v
     if (bytes) *bytes = (size_t)off;
     if (!buffer) return BMFR_OK;
     return hip_status(bmfr::launch_halo_copy(a, as_stream(stream), buffer, unpack));
+}
+
+bmfr_status bmfr_halo_need(const bmfr_config* cfg, int frame_number, int state_rect[4], int result_rect[4]) {
+    if (!cfg || frame_number < 0 || !state_rect || !result_rect) return BMFR_ERROR_INVALID_ARGUMENT;
+    bmfr_sizes sz;
+    const bmfr_status st = bmfr_config_sizes(cfg, &sz);
+    if (st != BMFR_OK) return st;
+    if (!is_tiled(cfg)) return BMFR_ERROR_UNSUPPORTED;
+    const Params P = frame_params_cfg(*cfg, make_params(cfg, &sz), frame_number);
+    const int v[4] = {P.vx0, P.vy0, P.vx1 - P.vx0, P.vy1 - P.vy0}, w[4] = {P.wx0, P.wy0, P.wx1 - P.wx0, P.wy1 - P.wy0};
+    for (int k = 0; k < 4; ++k) state_rect[k] = v[k], result_rect[k] = w[k];
+    return BMFR_OK;
 }
 
 bmfr_status bmfr_set_profiling_stride(bmfr_ctx* c, int stride) {

@@ -92,6 +92,7 @@ struct NoisyItem {
     float alpha_f;
     bool prev_f_divided;  // the tap weights summed to > 0 (alpha_f from spp)
     int over;             // noisy_item_spec, P.check_reach: px by which an in-image tap leaves [vx0, vx1) x [vy0, vy1)
+                          // ([wx0, wx1) x [wy0, wy1) for a pixel of the output tile)
 };
 
 struct NoisyInputs {
@@ -320,8 +321,12 @@ __device__ __forceinline__ NoisyTaps noisy_taps_issue(const Params& P, const Noi
         if (P.check_reach) {  // the in-image taps span [x0, x1] x [y0, y1]
             const int x0 = max(ix, 0), x1 = min(ix + 1, P.width - 1);
             const int y0 = max(iy, 0), y1 = min(iy + 1, P.height - 1);
+            // a tile pixel's taps also read the previous TAA output (in K2)
+            const bool tpx = c.px >= P.tx0 && c.px < P.tx1 && c.py >= P.ty0 && c.py < P.ty1;
+            const int vx0 = tpx ? P.wx0 : P.vx0, vx1 = tpx ? P.wx1 : P.vx1;
+            const int vy0 = tpx ? P.wy0 : P.vy0, vy1 = tpx ? P.wy1 : P.vy1;
             if (x0 <= x1 && y0 <= y1)
-                tp.over = max(max(max(P.vx0 - x0, x1 - (P.vx1 - 1)), max(P.vy0 - y0, y1 - (P.vy1 - 1))), 0);
+                tp.over = max(max(max(vx0 - x0, x1 - (vx1 - 1)), max(vy0 - y0, y1 - (vy1 - 1))), 0);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {

@@ -54,8 +54,12 @@ struct Params {
     // halo exchange (interior blocks), the region after it.  K1 reports the
     // largest distance by which an in-image reprojection tap (bmfr.cl:374-419)
     // falls outside it (include/bmfr.h: BMFR_ERROR_HALO_EXCEEDED).
+    // [wx0, wx1) x [wy0, wy1): where the previous TAA output is valid -- it
+    // bounds the taps of the tile's own pixels, which K2 reuses for its
+    // bilinear read of that output (bmfr.cl:924-944).
     int check_reach;
     int vx0, vy0, vx1, vy1;
+    int wx0, wy0, wx1, wy1;
 };
 
 // BLOCK_OFFSETS (bmfr.cl:267-285), host copy of the device table in

@@ -11,7 +11,11 @@ exactly that: for every pair of ranks, the part of the sender's tile that
 lies inside the receiver's region, for the four state planes the next frame
 reads (accumulated noisy colour, spp, accumulated filtered colour, TAA
 output).  Current-frame inputs need no exchange: each rank reads (renders)
-its own region.
+its own region.  What a frame reads of that ring is narrower
+(`bmfr_halo_need`, include/bmfr.h): the three accumulation planes over the
+pixels of the frame's K1 blocks grown by the reprojection reach, the TAA
+output over the tile grown by the reach -- so `frame_plan` sends only those
+parts (per frame: the block grid shifts with frame % 16).
 
 Transports: `DistTransport` (torch.distributed point-to-point; RCCL over
 xGMI with the nccl backend, gloo on CPU) and `LoopbackTransport` (all tiles
@@ -21,10 +25,14 @@ from __future__ import annotations
 
 import ctypes as C
 import dataclasses
+import functools
 
 # (plane name in bmfr_state_view, bytes per pixel)
 STATE_PLANES = (("noisy_accumulated", 12), ("spp", 1), ("filtered_accumulated", 12), ("result", 12))
 MIN_HALO = 34  # include/bmfr.h: blocks reach 32 px past the tile, + TAA and bilinear taps
+# plane masks of bmfr_halo_copy rectangles (include/bmfr.h BMFR_HALO_*)
+HALO_STATE, HALO_RESULT = 1 | 2 | 4, 8
+HALO_ALL = HALO_STATE | HALO_RESULT
 
 
 def _split(n: int, parts: int, i: int) -> tuple[int, int]:
@@ -56,6 +64,26 @@ def intersect(a: Rect, b: Rect) -> Rect | None:
     return (x0, y0, x1 - x0, y1 - y0) if x1 > x0 and y1 > y0 else None
 
 
+@functools.lru_cache(maxsize=None)
+def _need(width, height, tile, halo, frame16):
+    """bmfr_halo_need for one tile: (state_rect, result_rect)."""
+    from . import _lib
+    from .pipeline import BmfrConfig
+    cfg = BmfrConfig(image_width=width, image_height=height, tile=tile, tile_halo=halo).to_c()
+    st, rs = (C.c_int * 4)(), (C.c_int * 4)()
+    _lib.check(_lib.load().bmfr_halo_need(C.byref(cfg), frame16, st, rs), "bmfr_halo_need")
+    return tuple(st), tuple(rs)
+
+
+def _masked(part_of: Rect, state: Rect, result: Rect) -> list:
+    """The parts of `part_of` inside the state / result rectangles, as
+    bmfr_halo_copy records (x, y, w, h, planes)."""
+    s, r = intersect(part_of, state), intersect(part_of, result)
+    if s and s == r:
+        return [(*s, HALO_ALL)]
+    return ([(*s, HALO_STATE)] if s else []) + ([(*r, HALO_RESULT)] if r else [])
+
+
 @dataclasses.dataclass(frozen=True)
 class TileGrid:
     """A width x height frame cut into tiles_x x tiles_y tiles (rank = ty * tiles_x + tx)."""
@@ -84,6 +112,25 @@ class TileGrid:
         x0, y0 = max(0, x - self.halo), max(0, y - self.halo)
         x1, y1 = min(self.width, x + w + self.halo), min(self.height, y + h + self.halo)
         return (x0, y0, x1 - x0, y1 - y0)
+
+    def need(self, rank: int, frame: int):
+        """(state_rect, result_rect): what `rank`'s frame `frame` reads of the
+        previous state (bmfr_halo_need)."""
+        return _need(self.width, self.height, self.tile(rank), self.halo, frame % 16)
+
+    def frame_plan(self, rank: int, frame: int):
+        """[(peer, send, recv)] for the exchange before `frame`: send = the
+        parts of my tile that the peer's frame reads, recv = the parts of the
+        peer's tile that mine reads, as bmfr_halo_copy records."""
+        out = []
+        for peer in range(self.ranks):
+            if peer == rank:
+                continue
+            send = _masked(self.tile(rank), *self.need(peer, frame))
+            recv = _masked(self.tile(peer), *self.need(rank, frame))
+            if send or recv:
+                out.append((peer, send, recv))
+        return out
 
     def plan(self, rank: int):
         """[(peer, send_rect, recv_rect)]: send the part of my tile inside the
@@ -170,19 +217,18 @@ def rect_bytes(planes, r: Rect | None) -> int:
 
 # ------------------------------------------------- libbmfr halo copies ----
 def _rect_array(rects):
-    return (C.c_int * max(4 * len(rects), 1))(*[v for r in rects for v in r])
+    """bmfr_halo_copy records: (x, y, w, h[, planes]) -> 5 ints each (all planes by default)."""
+    recs = [tuple(r) if len(r) == 5 else (*r, HALO_ALL) for r in rects]
+    return (C.c_int * max(5 * len(recs), 1))(*[v for r in recs for v in r])
 
 
-def halo_bytes(denoiser, rects) -> list:
-    """Packed size of each rectangle's four state-plane segments (bmfr_halo_copy layout)."""
+def halo_bytes(denoiser, rects) -> int:
+    """Packed size of the rectangles' segments (bmfr_halo_copy layout)."""
     from ._lib import check
-    out = []
-    for r in rects:
-        n = C.c_size_t()
-        check(denoiser.lib.bmfr_halo_copy(denoiser.handle, None, _rect_array([r]), 1, None, 0, C.byref(n)),
-              "bmfr_halo_copy")
-        out.append(n.value)
-    return out
+    n = C.c_size_t()
+    check(denoiser.lib.bmfr_halo_copy(denoiser.handle, None, _rect_array(rects), len(rects), None, 0, C.byref(n)),
+          "bmfr_halo_copy")
+    return n.value
 
 
 def halo_copy(denoiser, rects, buf_ptr: int, unpack: bool, stream=None) -> None:
@@ -211,6 +257,8 @@ class DistTransport:
         self.grid, self.rank, self.device = grid, rank, device
         self.host_staging = host_staging
         self._bufs = {}
+        self._layouts = {}
+        self.last_bytes = (0, 0)
 
     def buffer(self, key, nbytes, device=None):
         b = self._bufs.get(key)
@@ -219,24 +267,27 @@ class DistTransport:
             self._bufs[key] = b
         return b
 
-    def exchange_ctx(self, denoiser) -> None:
-        """The exchange on a tiled Denoiser with libbmfr's one-launch pack and
-        unpack (bmfr_halo_copy) on the current stream: two kernels per frame
-        around one grouped isend/irecv batch (RCCL orders it on that stream)."""
+    def exchange_ctx(self, denoiser, frame: int) -> None:
+        """The exchange before `frame` on a tiled Denoiser (TileGrid.frame_plan)
+        with libbmfr's one-launch pack and unpack (bmfr_halo_copy) on the
+        current stream: two kernels around one grouped isend/irecv batch
+        (RCCL orders it on that stream).  self.last_bytes = (sent, received)."""
         import torch.distributed as dist
-        if not hasattr(self, "_layout"):
-            plan = self.grid.plan(self.rank)
+        key = frame % 16
+        if key not in self._layouts:
+            plan = self.grid.frame_plan(self.rank, frame)
             sends = [(p, s) for p, s, _ in plan if s]
             recvs = [(p, r) for p, _, r in plan if r]
-            self._layout = (sends, halo_bytes(denoiser, [s for _, s in sends]),
-                            recvs, halo_bytes(denoiser, [r for _, r in recvs]))
-        sends, s_sizes, recvs, r_sizes = self._layout
+            self._layouts[key] = (sends, [halo_bytes(denoiser, s) for _, s in sends],
+                                  recvs, [halo_bytes(denoiser, r) for _, r in recvs])
+        sends, s_sizes, recvs, r_sizes = self._layouts[key]
+        ns, nr = sum(s_sizes), sum(r_sizes)
+        self.last_bytes = (ns, nr)
         if not sends and not recvs:
             return
-        ns, nr = sum(s_sizes), sum(r_sizes)
         sbuf = self.buffer("S", ns)
         rbuf = self.buffer("R", nr)
-        halo_copy(denoiser, [s for _, s in sends], sbuf.data_ptr(), unpack=False)
+        halo_copy(denoiser, [q for _, s in sends for q in s], sbuf.data_ptr(), unpack=False)
         s_msg, r_msg = sbuf, rbuf
         if self.host_staging:  # gloo: the messages travel through host memory
             cpu = self.torch.device("cpu")
@@ -254,7 +305,7 @@ class DistTransport:
             w.wait()
         if self.host_staging:
             rbuf[:nr].copy_(r_msg[:nr])
-        halo_copy(denoiser, [r for _, r in recvs], rbuf.data_ptr(), unpack=True)
+        halo_copy(denoiser, [q for _, r in recvs for q in r], rbuf.data_ptr(), unpack=True)
 
     def exchange(self, planes, copier) -> None:
         import torch.distributed as dist
@@ -295,19 +346,18 @@ class LoopbackTransport:
     def __init__(self, grid: TileGrid):
         self.grid = grid
 
-    def exchange_all_ctx(self, denoisers) -> None:
-        """The same through libbmfr's pack / unpack kernels (bmfr_halo_copy):
-        each message packed from the sender's context and unpacked into the
-        receiver's, as DistTransport.exchange_ctx moves them."""
+    def exchange_all_ctx(self, denoisers, frame: int) -> None:
+        """The exchange before `frame` through libbmfr's pack / unpack kernels
+        (bmfr_halo_copy): each message packed from the sender's context and
+        unpacked into the receiver's, as DistTransport.exchange_ctx moves them."""
         import torch
         for rank in range(self.grid.ranks):
-            for peer, s, _ in self.grid.plan(rank):
+            for peer, s, _ in self.grid.frame_plan(rank, frame):
                 if not s:
                     continue
-                n = halo_bytes(denoisers[rank], [s])[0]
-                buf = torch.empty(n, dtype=torch.uint8, device="cuda")
-                halo_copy(denoisers[rank], [s], buf.data_ptr(), unpack=False)
-                halo_copy(denoisers[peer], [s], buf.data_ptr(), unpack=True)
+                buf = torch.empty(halo_bytes(denoisers[rank], s), dtype=torch.uint8, device="cuda")
+                halo_copy(denoisers[rank], s, buf.data_ptr(), unpack=False)
+                halo_copy(denoisers[peer], s, buf.data_ptr(), unpack=True)
 
     def exchange_all(self, planes_by_rank, copier) -> None:
         for rank in range(self.grid.ranks):

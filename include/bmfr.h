@@ -88,7 +88,7 @@ typedef struct bmfr_config {
      * frame > 0 the caller refreshes the region's halo ring of the state
      * planes (noisy_accumulated, spp, filtered_accumulated, result of
      * bmfr_state(previous = 0)) from the neighbouring tiles, which own those
-     * pixels.  Exact for scene motion below tile_halo - 34 pixels per frame
+     * pixels -- at least the parts bmfr_halo_need names for that frame.  Exact for scene motion below tile_halo - 34 pixels per frame
      * (32: blocks reaching past the tile, 2: TAA + bilinear taps); the
      * reference reprojects to any pixel (bmfr.cl:343-356), so the kernels
      * check it: a frame whose reprojection taps reach past the state that
@@ -242,16 +242,36 @@ bmfr_status bmfr_process_sequence(bmfr_ctx *ctx, void *stream, int count, const 
     const float *prev_frame_camera_matrices, const float *pixel_offsets, int first_frame,
     float *const *outputs);
 
-/* Halo exchange support for tiled contexts: copy the rectangles rects[n][4]
- * = {x, y, width, height} (image coordinates inside the context's region) of
- * the four exchanged state planes of bmfr_state(previous = 0) --
- * noisy_accumulated (12 B/px), spp (1), filtered_accumulated (12), result
- * (12) -- into (unpack = 0) or out of (unpack = 1) `buffer` (device memory),
- * rectangle after rectangle, plane after plane, rows packed, each segment
- * padded to 16 bytes; one kernel launch on `stream`.  *bytes (nullable)
- * receives the packed size; buffer = NULL only computes it.  n <= 16. */
+/* Halo exchange support for tiled contexts: copy the rectangles rects[n][5]
+ * = {x, y, width, height, planes} (image coordinates inside the context's
+ * region; planes = a non-empty mask of BMFR_HALO_*) of the exchanged state
+ * planes of bmfr_state(previous = 0) -- noisy_accumulated (12 B/px), spp
+ * (1), filtered_accumulated (12), result (12) -- into (unpack = 0) or out of
+ * (unpack = 1) `buffer` (device memory), rectangle after rectangle, plane
+ * after plane in that order, rows packed, each segment padded to 16 bytes;
+ * one kernel launch on `stream`.  *bytes (nullable) receives the packed
+ * size; buffer = NULL only computes it.  At most 64 segments (rectangle x
+ * plane). */
+#define BMFR_HALO_NOISY 1
+#define BMFR_HALO_SPP 2
+#define BMFR_HALO_FILTERED 4
+#define BMFR_HALO_RESULT 8
+#define BMFR_HALO_STATE (BMFR_HALO_NOISY | BMFR_HALO_SPP | BMFR_HALO_FILTERED)
+#define BMFR_HALO_ALL (BMFR_HALO_STATE | BMFR_HALO_RESULT)
 bmfr_status bmfr_halo_copy(bmfr_ctx *ctx, void *stream, const int *rects, int n, void *buffer, int unpack,
     size_t *bytes);
+
+/* What frame `frame_number` of a tiled configuration reads of the previous
+ * frame's state ({x, y, width, height}, inside the region; host only, no
+ * context): state_rect for noisy_accumulated / spp / filtered_accumulated --
+ * the pixels of the frame's K1 blocks (its shifted block grid, bmfr.cl:
+ * 267-285; mirrored at the frame border) grown by tile_halo - 33 --, and
+ * result_rect for the TAA output -- the tile grown by tile_halo - 33.
+ * Before frame_number the caller must refresh the parts of these
+ * rectangles outside the tile (refreshing the whole halo ring is also
+ * correct); the kernels check the reprojection taps against them.  Both
+ * depend on frame_number % 16 only. */
+bmfr_status bmfr_halo_need(const bmfr_config *cfg, int frame_number, int state_rect[4], int result_rect[4]);
 
 /* Tiled contexts: waits for the last enqueued frame and returns
  * BMFR_ERROR_HALO_EXCEEDED if any frame since frame 0 read reprojection taps

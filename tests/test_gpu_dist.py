@@ -51,7 +51,7 @@ def _worker(rank, world, port, q):
                 comm.wait_event(done)
                 den.process_frame_interior(*args, **kw)
                 with torch.cuda.stream(comm):
-                    transport.exchange_ctx(den)
+                    transport.exchange_ctx(den, f)
                 compute.wait_stream(comm)
                 den.process_frame_border(*args, **kw)
             done.record(compute)

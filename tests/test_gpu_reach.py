@@ -50,12 +50,12 @@ def run(dx: float, frames: int = 3, split: bool = True):
         if split and f > 0:
             for r in range(grid.ranks):
                 tiles[r].process_frame_interior(*args[r], **kws[r])
-            loop.exchange_all_ctx(tiles)
+            loop.exchange_all_ctx(tiles, f)
             for r in range(grid.ranks):
                 tiles[r].process_frame_border(*args[r], **kws[r])
         else:
             if f > 0:
-                loop.exchange_all_ctx(tiles)
+                loop.exchange_all_ctx(tiles, f)
             for r in range(grid.ranks):
                 tiles[r].process_frame(*args[r], **kws[r])
         prev = inps

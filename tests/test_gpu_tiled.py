@@ -70,7 +70,7 @@ def test_tiled_matches_untiled_bitwise(shape, half, split, kernel_copy, gpu):
                 call("process_frame_interior", r)
             if f > 0:
                 if kernel_copy:  # libbmfr's one-launch pack / unpack (bmfr_halo_copy)
-                    loop.exchange_all_ctx(tiles)
+                    loop.exchange_all_ctx(tiles, f)
                 else:
                     loop.exchange_all([state_planes(d) for d in tiles], copier)
             for r in range(grid.ranks):
@@ -136,7 +136,7 @@ def test_8k_tiled_4x2_matches_untiled(gpu):
         else:
             for r in range(grid.ranks):
                 tiles[r].process_frame_interior(*args[r], **kws[r])
-            loop.exchange_all_ctx(tiles)
+            loop.exchange_all_ctx(tiles, f)
             for r in range(grid.ranks):
                 tiles[r].process_frame_border(*args[r], **kws[r])
         prev = inps

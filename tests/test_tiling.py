@@ -50,6 +50,76 @@ def test_tiles_partition_and_plan_is_symmetric(shape):
         assert reg.sum() == rw * rh
 
 
+OFFSETS = [(-14, -14), (4, -6), (-8, 14), (8, 0), (-10, -8), (2, 12), (12, -12), (-10, 0),
+           (12, 14), (-8, -16), (6, 6), (-2, -2), (6, -14), (-16, 12), (14, -4), (-6, 4)]  # bmfr.cl:267-285
+
+
+def _need_restated(g, rank, frame):
+    """bmfr_halo_need restated: blocks of frame's shifted grid reaching the
+    tile + 1 px, their mirrored pixels grown by halo - 33; the tile grown by
+    the same; clipped to the region."""
+    x, y, w, h = g.tile(rank)
+    rx, ry, rw, rh = g.region(rank)
+    reach = g.halo - 33
+    out_s, out_r = [], []
+    for t0, t1, size, off, r0, r1 in ((x, x + w, g.width, OFFSETS[frame % 16][0], rx, rx + rw),
+                                      (y, y + h, g.height, OFFSETS[frame % 16][1], ry, ry + rh)):
+        nb = (32 * ((size + 31) // 32) + 32) // 32
+        lo, hi = size, -1
+        for b in range(nb):
+            p0 = 32 * b - 16 + off
+            if p0 < min(size, t1 + 1) and p0 + 32 > max(0, t0 - 1):
+                for p in range(p0, p0 + 32):
+                    m = -p - 1 if p < 0 else (2 * size - p - 1 if p >= size else p)
+                    lo, hi = min(lo, m), max(hi, m)
+        out_s.append((max(lo - reach, r0), min(hi + 1 + reach, r1)))
+        out_r.append((max(t0 - reach, r0), min(t1 + reach, r1)))
+    rect = lambda a: (a[0][0], a[1][0], a[0][1] - a[0][0], a[1][1] - a[1][0])  # noqa: E731
+    return rect(out_s), rect(out_r)
+
+
+@pytest.mark.parametrize("shape", [(7680, 4320, 4, 2, 64), (3840, 2160, 2, 2, 40), (480, 288, 4, 2, 38),
+                                   (320, 256, 2, 2, 40), (1000, 700, 1, 4, 50)])
+def test_frame_plan_sends_what_each_frame_reads(shape):
+    """The per-frame exchange (bmfr_halo_need, TileGrid.frame_plan): the C ABI
+    equals the restatement; the result rectangle lies inside the state one,
+    which lies inside the region and covers the tile + 1 px; every rank
+    receives exactly the parts of its need rectangles outside its tile, each
+    from the peer that owns them; the plan is symmetric; and it moves fewer
+    bytes than the whole halo ring."""
+    W, H, tx, ty, halo = shape
+    g = TileGrid(W, H, tx, ty, halo=halo)
+    bpp = {1: 12, 2: 1, 4: 12, 8: 12}
+    for frame in range(1, 17):
+        ring_bytes = plan_bytes = 0
+        for r in range(g.ranks):
+            st, rs = g.need(r, frame)
+            assert (st, rs) == _need_restated(g, r, frame)
+            x, y, w, h = g.tile(r)
+            assert intersect(st, rs) == rs and intersect(g.region(r), st) == st
+            assert intersect(st, (x - 1, y - 1, w + 2, h + 2)) == intersect((0, 0, W, H), (x - 1, y - 1, w + 2, h + 2))
+            plan = g.frame_plan(r, frame)
+            back = {p: (s2, r2) for p, s2, r2 in []}
+            for peer, send, recv in plan:
+                back = {p: (s2, r2) for p, s2, r2 in g.frame_plan(peer, frame)}
+                assert back[r][0] == recv and back[r][1] == send
+            for k, need in ((1, st), (8, rs)):
+                got = np.zeros((H, W), np.int32)
+                for peer, _, recv in plan:
+                    pt = g.tile(peer)
+                    for (qx, qy, qw, qh, m) in recv:
+                        if m & k:
+                            assert intersect(pt, (qx, qy, qw, qh)) == (qx, qy, qw, qh)
+                            got[qy:qy + qh, qx:qx + qw] += 1
+                want = np.zeros((H, W), np.int32)
+                want[need[1]:need[1] + need[3], need[0]:need[0] + need[2]] = 1
+                want[y:y + h, x:x + w] = 0
+                assert (got == want).all(), (frame, r, k)
+            ring_bytes += sum(rect_bytes([Plane(0, g.region(r), b) for _, b in STATE_PLANES], rc) for _, _, rc in g.plan(r))
+            plan_bytes += sum(q[2] * q[3] * sum(bpp[b] for b in bpp if q[4] & b) for _, _, recv in plan for q in recv)
+        assert plan_bytes < ring_bytes
+
+
 def _truth(name, bpp, W, H):
     """Deterministic per-plane content of the whole frame (bytes)."""
     idx = np.arange(W * H * bpp, dtype=np.uint64).reshape(H, W * bpp)
