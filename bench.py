@@ -201,7 +201,7 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
         _, jit = bmfr_amd.synth_camera(W, H, f)
         cams.append((vp, jit))
-    spin_up(a, cfg, local, frames, cams)
+    scratch = spin_up(a, cfg, local, frames, cams)  # its last frames still run under the warm-up frames
     transport = tiling.DistTransport(grid, rank, dev, host_staging=backend != "nccl") if grid else None
     # Tiled: the halo exchange runs on its own stream while K1's interior
     # blocks (which need no halo) run on the compute stream
@@ -212,7 +212,6 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     # Split timings of sampled timed frames: (interior start/end, exchange
     # start/end, border end) events, on the streams the work runs on.
     marks = []
-    torch.cuda.synchronize()
 
     def run(f, mark=False):
         fr = frames[f]
@@ -339,7 +338,7 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         "psnr_in": psnr(tile_of(noisy_tm).cpu().numpy(), tile_of(clean).cpu().numpy()),
         "split": split,
     }
-    del frames, den, out, clean, noisy_tm, last
+    del frames, den, out, clean, noisy_tm, last, scratch
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return res
@@ -377,27 +376,33 @@ def side_line(r):
             "psnr_db": round(r["psnr"], 2)}
 
 
-def spin_up(a, cfg, local, frames, cams) -> None:
+def spin_up(a, cfg, local, frames, cams):
     """Untimed: the same frames through a scratch context for --spin-up
-    seconds before the measured context starts.  The GPU's shader clock
-    follows its load -- in-kernel timestamps (tools/k1_phases.py: block
-    cycles over the 100 MHz real-time counter) put it at 1.7 GHz in the
-    first frames of a run and 2.3 GHz after ~100 frames of this workload --
-    so the warm-up is this workload, not a different kernel.  A tiled
-    scratch context runs without the halo exchange (its results are
-    discarded)."""
+    seconds before the measured context starts; returns that context, whose
+    last frames are still in flight (the caller keeps it alive until after
+    the timed region).  The GPU's power management sets the shader clock by
+    the load: in-kernel timestamps (tools/k1_phases.py: block cycles over the
+    100 MHz real-time counter) read 1.5-1.9 GHz for the first ~30 frames
+    after the GPU idled for a few milliseconds, 2.2-2.3 GHz in steady
+    state -- so the warm-up is this workload, and it hands over to the
+    warm-up frames of the measured context without the GPU going idle
+    (tools/frame_times.py: passes enqueued back to back have no slow early
+    frames).  A tiled scratch context runs without the halo exchange (its
+    results are discarded)."""
     if a.spin_up <= 0:
-        return
+        return None
     scratch = bmfr_amd.Denoiser(cfg, device=local)
     t0, f = time.perf_counter(), 0
-    while time.perf_counter() - t0 < a.spin_up:
+    while True:
         for _ in range(8):
-            fr = frames[f % len(frames)]
-            scratch.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"],
-                                  cams[f % len(frames)][0], cams[f % len(frames)][1], f % len(frames))
+            g = f % len(frames)
+            fr = frames[g]
+            scratch.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], cams[g][0], cams[g][1],
+                                  g)
             f += 1
+        if time.perf_counter() - t0 >= a.spin_up:
+            return scratch
         torch.cuda.synchronize()
-    del scratch
 
 
 def main():

@@ -27,13 +27,17 @@ cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H)
 den = bmfr_amd.Denoiser(cfg)
 G = den.sizes.blocks
 names = ["accumulate_noisy", "min/max scale", "QR", "back-subst", "weighted+blend"]
-for f in range(max(report) + 1):
-    fr = bmfr_amd.synth_frame_device(W, H, f)
-    vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
-    _, jit = bmfr_amd.synth_camera(W, H, f)
-    den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, f)
-    if f not in report:
+# frames rendered up front; a first pass over them untimed (GPU at its working clock)
+frames = [bmfr_amd.synth_frame_device(W, H, f) for f in range(max(report) + 1)]
+for f in range(len(frames) * 2):
+    fr = frames[f % len(frames)]
+    g = f % len(frames)
+    vp, _ = bmfr_amd.synth_camera(W, H, max(g - 1, 0))
+    _, jit = bmfr_amd.synth_camera(W, H, g)
+    den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, g)
+    if f < len(frames) or g not in report:
         continue
+    f = g
     torch.cuda.synchronize()
     buf = np.zeros(G * 8, np.uint64)
     rc = den.lib.bmfr_debug_stamps(den.handle, buf.ctypes.data_as(C.c_void_p), buf.size)
