@@ -155,3 +155,67 @@ def test_8k_tiled_4x2_matches_untiled(gpu):
                 b = v[y:y + h, x:x + w].contiguous().view(torch.int32)
                 assert torch.equal(a, b), (f, r, k, int((a != b).sum()))
         del want
+
+
+def test_halo_copy_plane_masks(gpu):
+    """bmfr_halo_copy records {x, y, w, h, planes}: each mask packs exactly
+    its planes (segment sizes padded to 16 bytes), a pack / unpack round trip
+    through another context moves only those planes, and masks outside
+    1..15 are rejected."""
+    import ctypes as C
+
+    from bmfr_amd import tiling
+    W, H = 320, 256
+    grid = TileGrid(W, H, 2, 2, halo=40)
+    a, b = (bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H, tile=grid.tile(r), tile_halo=40))
+            for r in (0, 1))
+    # rectangle of tile 0 inside region 1
+    rect = tiling.intersect(grid.tile(0), grid.region(1))
+    assert rect is not None
+    n = rect[2] * rect[3]
+    pad = lambda x: (x + 15) // 16 * 16  # noqa: E731
+    sizes = {1: 12 * n, 2: n, 4: 12 * n, 8: 12 * n}
+    for mask in range(1, 16):
+        want = sum(pad(v) for k, v in sizes.items() if mask & k)
+        assert tiling.halo_bytes(a, [(*rect, mask)]) == want
+    for bad in (0, 16, -1):
+        with pytest.raises(bmfr_amd.BmfrError):
+            tiling.halo_bytes(a, [(*rect, bad)])
+    # one frame so both contexts hold state; then move only the spp and result planes
+    for d in (a, b):
+        inp = bmfr_amd.synth_region_device(W, H, d.region, 0)
+        vp, jit = bmfr_amd.synth_camera(W, H, 0)
+        d.process_frame(inp["noisy"], inp["normals"], inp["positions"], inp["albedo"], vp, jit, 0)
+    torch.cuda.synchronize()
+
+    def planes(d):
+        m = d.region[2] * d.region[3]
+        return {k: (d.copy_output(torch.empty(3 * m, device="cuda")) if k == "result" else
+                    d.copy_state(k, torch.empty(m if k == "spp" else 3 * m,
+                                                dtype=torch.uint8 if k == "spp" else torch.float32, device="cuda")))
+                .cpu().numpy().copy() for k in ("noisy_accumulated", "spp", "filtered_accumulated", "result")}
+
+    before_a, before_b = planes(a), planes(b)
+    recs = [(*rect, 2 | 8)]
+    buf = torch.empty(tiling.halo_bytes(a, recs), dtype=torch.uint8, device="cuda")
+    tiling.halo_copy(a, recs, buf.data_ptr(), unpack=False)
+    tiling.halo_copy(b, recs, buf.data_ptr(), unpack=True)
+    torch.cuda.synchronize()
+    after_b = planes(b)
+    ra, rb = a.region, b.region
+    x, y, w, h = rect
+    for k in before_b:
+        ch = 1 if k == "spp" else 3
+        va = before_a[k].reshape(ra[3], ra[2], ch)[y - ra[1]:y - ra[1] + h, x - ra[0]:x - ra[0] + w]
+        vb0 = before_b[k].reshape(rb[3], rb[2], ch)
+        vb1 = after_b[k].reshape(rb[3], rb[2], ch)
+        inside = vb1[y - rb[1]:y - rb[1] + h, x - rb[0]:x - rb[0] + w]
+        if k in ("spp", "result"):
+            assert inside.tobytes() == va.tobytes(), k
+        else:
+            assert vb1.tobytes() == vb0.tobytes(), k  # untouched plane
+        outside = vb1.copy()
+        outside[y - rb[1]:y - rb[1] + h, x - rb[0]:x - rb[0] + w] = 0
+        ref = vb0.copy()
+        ref[y - rb[1]:y - rb[1] + h, x - rb[0]:x - rb[0] + w] = 0
+        assert outside.tobytes() == ref.tobytes(), k
