@@ -490,7 +490,9 @@ def main():
             roof = {"bound": "hbm", "achieved": round(fa, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(fa / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(workload + "_frame"),
                     "kernel": "k_fused_cols_taa<..., SAME = true> (K1 + K2 of the frame, one launch)",
-                    "algorithmic_bytes_per_launch": fb, "launch_ms": round(r["frame_kernel_ms"], 4)}
+                    "algorithmic_bytes_per_launch": fb, "launch_ms": round(r["frame_kernel_ms"], 4),
+                    "limiter": "K1 blocks: latency of phase-1 gathers and of the fit's pivot chain, VALU issue "
+                               "(roofline_k1); TAA tiles: texture path / latency (roofline_k2) -- not HBM"}
         else:
             roof = k1_roof
         roof["frame_frac"] = round(frame_bytes_per_px(s) * W * H / (ms_per_frame * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
