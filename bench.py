@@ -117,6 +117,9 @@ def parse():
                     help="multi-GPU: strong = one --width x --height frame split (default), "
                          "weak = one --width x --height tile per GPU")
     ap.add_argument("--halo", type=int, default=64, help="tile halo in pixels (>= 34 + max motion)")
+    ap.add_argument("--grid", default=None,
+                    help="multi-GPU tile grid COLSxROWS (default: 2x1, 2x2, 4x2 for N = 2, 4, 8 -- the 4x2 tiles "
+                         "of 8K are 1920x2160, a shorter halo perimeter than 2x4's 3840x1080)")
     ap.add_argument("--sequence", action="store_true",
                     help="single GPU: the timed frames as one bmfr_process_sequence call (TAA of frame f beside "
                          "K1 of frame f+1) instead of one bmfr_process_frame per frame")
@@ -424,7 +427,9 @@ def main():
     a.width = a.width or (3840 if world == 1 else 7680)
     a.height = a.height or (2160 if world == 1 else 4320)
 
-    tx, ty = tiling.grid_for(world)
+    tx, ty = tiling.grid_for(world) if not a.grid else tuple(int(v) for v in a.grid.lower().split("x"))
+    if tx * ty != world:
+        raise SystemExit(f"--grid {a.grid}: {tx * ty} tiles for {world} ranks")
     if a.scaling == "weak":
         W, H = a.width * tx, a.height * ty
     else:

@@ -78,7 +78,7 @@ def _need_restated(g, rank, frame):
     return rect(out_s), rect(out_r)
 
 
-@pytest.mark.parametrize("shape", [(7680, 4320, 4, 2, 64), (3840, 2160, 2, 2, 40), (480, 288, 4, 2, 38),
+@pytest.mark.parametrize("shape", [(7680, 4320, 4, 2, 64), (7680, 4320, 2, 4, 64), (3840, 2160, 2, 2, 40), (480, 288, 4, 2, 38),
                                    (320, 256, 2, 2, 40), (1000, 700, 1, 4, 50)])
 def test_frame_plan_sends_what_each_frame_reads(shape):
     """The per-frame exchange (bmfr_halo_need, TileGrid.frame_plan): the C ABI
