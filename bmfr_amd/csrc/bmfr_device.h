@@ -103,6 +103,33 @@ __device__ __forceinline__ f3 ld3in(const float* __restrict__ b, uint32_t i) {
     }
 }
 
+// The same pixel as loaded (In3<float> = f3, In3<_Float16> = the 6 bytes),
+// widened by widen() where it is used: a conversion right after a load makes
+// the wave wait for that load, so the loads a pipeline stage issues together
+// stay raw until the stage consumes them.
+template <class IN>
+struct In3 {
+    f3 v;
+};
+struct __attribute__((packed, aligned(2))) h3raw {  // h3mem's bytes: x | y << 16, z
+    uint32_t xy;
+    uint16_t z;
+};
+template <>
+struct In3<_Float16> {
+    h3raw v;  // kept whole (not split into halves) until widened
+};
+template <class IN>
+__device__ __forceinline__ In3<IN> ld3raw(const float* __restrict__ b, uint32_t i) {
+    if constexpr (sizeof(IN) == 2) return In3<IN>{*reinterpret_cast<const h3raw*>(at_byte(b, i * 6u))};
+    else return In3<IN>{ld3(b, i)};
+}
+__device__ __forceinline__ f3 widen(const In3<float>& r) { return r.v; }
+__device__ __forceinline__ f3 widen(const In3<_Float16>& r) {
+    return f3{(float)__builtin_bit_cast(_Float16, (uint16_t)(r.v.xy & 0xffffu)),
+              (float)__builtin_bit_cast(_Float16, (uint16_t)(r.v.xy >> 16)), (float)__builtin_bit_cast(_Float16, r.v.z)};
+}
+
 // OpenCL dot() as ROCm's opencl.bc implements it (fmuladd chain).
 __device__ __forceinline__ float dot3(f3 a, f3 b) {
     return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));

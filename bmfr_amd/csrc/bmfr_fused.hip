@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
     int over = 0;
     uint32_t state = 0;  // per s: owner (bit 0), accept bits (1-4), spp (8-15) -> 16 bits each ...
     uint32_t state_hi = 0;
-    NoisyCur cur[kSubs];  // current-frame loads of all four rows go out first
+    NoisyCur<IN> cur[kSubs];  // current-frame loads of all four rows go out first
 #pragma unroll
     for (int s = 0; s < kSubs; ++s)
         cur[s] = noisy_load_current<IN>(P, in, bx * kEdge + (t & (kEdge - 1)), by * kEdge + (t >> 5) + 8 * s, frame);

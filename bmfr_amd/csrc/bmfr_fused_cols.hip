@@ -535,14 +535,14 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // Software-pipelined one item deep: item i + 1's current-frame loads go
     // out right behind item i's reprojection taps, so each wait for taps
     // leaves the next item's loads in flight.
-    NoisyCur cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly, frame);
+    NoisyCur<IN> cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly, frame);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const NoisyTaps tp = noisy_taps_issue<true, IN>(P, A.in, A.cam, cur, frame, A.acc_prev);
-        NoisyCur nxt;
+        const NoisyTaps<IN> tp = noisy_taps_issue<true, IN>(P, A.in, A.cam, cur, frame, A.acc_prev);
+        NoisyCur<IN> nxt;
         if (i < 3) nxt = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly + 2 * (i + 1), frame);
         __builtin_amdgcn_sched_barrier(0);
-        const NoisyItem it = noisy_taps_finish<true>(P, cur, tp, frame);
+        const NoisyItem it = noisy_taps_finish<true, IN>(P, cur, tp, frame);
         {
 #pragma unroll
             for (int f = 1; f < B; ++f) {

@@ -249,24 +249,26 @@ __device__ __forceinline__ NoisyItem noisy_item(const Params& P, const NoisyInpu
 // unconditionally (out-of-image taps at a clamped in-image address, then
 // ignored), so a pixel costs two dependent memory round trips instead of up
 // to four.  The arithmetic, its order and the results are noisy_item's.
+// The current-frame planes of one item, as loaded (widened where used).
+template <class IN = float>
 struct NoisyCur {
-    f3 wp, nrm, cur;
+    In3<IN> wp, nrm, cur;
     int px, py;
     bool owner;
 };
 template <class IN = float>
-__device__ __forceinline__ NoisyCur noisy_load_current(const Params& P, const NoisyInputs& in, int gx, int gy,
-                                                       int frame) {
-    NoisyCur c;
+__device__ __forceinline__ NoisyCur<IN> noisy_load_current(const Params& P, const NoisyInputs& in, int gx, int gy,
+                                                           int frame) {
+    NoisyCur<IN> c;
     const int2 off = kBlockOffsets[frame & 15];
     const int ux = gx - kEdge / 2 + off.x, uy = gy - kEdge / 2 + off.y;
     c.px = mirror(ux, P.width);
     c.py = mirror(uy, P.height);
     c.owner = ux >= 0 && ux < P.width && uy >= 0 && uy < P.height;
     const uint32_t lin = pix(P, c.px, c.py);
-    c.wp = ld3in<IN>(in.p_cur, lin);
-    c.nrm = ld3in<IN>(in.n_cur, lin);
-    c.cur = ld3in<IN>(in.noisy_cur, lin);
+    c.wp = ld3raw<IN>(in.p_cur, lin);
+    c.nrm = ld3raw<IN>(in.n_cur, lin);
+    c.cur = ld3raw<IN>(in.noisy_cur, lin);
     return c;
 }
 
@@ -274,25 +276,30 @@ __device__ __forceinline__ NoisyCur noisy_load_current(const Params& P, const No
 // current-frame loads while this item's taps are in flight: _issue does the
 // reprojection (bmfr.cl:343-372) and issues the tap loads, _finish tests,
 // weighs and blends them (bmfr.cl:374-445).
+template <class IN = float>
 struct NoisyTaps {
-    f3 pp[4], pn[4], pc[4], pa[4];
-    float sp[4], wts[4];
+    In3<IN> pp[4], pn[4];  // previous position / normal (input planes), as loaded
+    f3 pc[4], pa[4];
+    // spp taps as loaded (u8 zero-extended): converted in _finish, so no
+    // conversion -- and no wait for the loads -- sits in the issue half
+    uint32_t spu[4];
+    float wts[4];
     uint32_t inb;  // bit i: tap i inside the image
     float pfx, pfy, flx, fly;
     int over;
 };
 
 template <bool FILT = false, class IN = float>
-__device__ __forceinline__ NoisyTaps noisy_taps_issue(const Params& P, const NoisyInputs& in, const Camera& cam,
-                                                     const NoisyCur& c, int frame,
-                                                     const float* __restrict__ acc_prev = nullptr) {
-    NoisyTaps tp;
+__device__ __forceinline__ NoisyTaps<IN> noisy_taps_issue(const Params& P, const NoisyInputs& in, const Camera& cam,
+                                                         const NoisyCur<IN>& c, int frame,
+                                                         const float* __restrict__ acc_prev = nullptr) {
+    NoisyTaps<IN> tp;
     tp.pfx = (float)c.px;
     tp.pfy = (float)c.py;
     tp.over = 0;
     tp.inb = 0;
     if (frame > 0) {
-        const f3 wp = c.wp;
+        const f3 wp = widen(c.wp);
         const float* M = cam.m;
         float u = dot4(M[0], M[4], M[8], M[12], wp.x, wp.y, wp.z, 1.f);
         float v = dot4(M[1], M[5], M[9], M[13], wp.x, wp.y, wp.z, 1.f);
@@ -333,25 +340,25 @@ __device__ __forceinline__ NoisyTaps noisy_taps_issue(const Params& P, const Noi
             const int sx = ix + (i & 1), sy = iy + (i >> 1);
             tp.inb |= (uint32_t)(sx >= 0 && sy >= 0 && sx < P.width && sy < P.height) << i;
             const uint32_t s = pix(P, clamp_rx(P, sx), clamp_ry(P, sy));
-            tp.pp[i] = ld3in<IN>(in.p_prev, s);
-            tp.pn[i] = ld3in<IN>(in.n_prev, s);
+            tp.pp[i] = ld3raw<IN>(in.p_prev, s);
+            tp.pn[i] = ld3raw<IN>(in.n_prev, s);
             tp.pc[i] = ld3(in.noisy_prev, s);
-            tp.sp[i] = (float)ld_px(in.spp_prev, s);
+            tp.spu[i] = ld_px(in.spp_prev, s);
             if (FILT) tp.pa[i] = ld3(acc_prev, s);  // same taps (bmfr.cl:801-832)
         }
     }
     return tp;
 }
 
-template <bool FILT = false>
-__device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const NoisyCur& c, const NoisyTaps& tp,
+template <bool FILT = false, class IN = float>
+__device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const NoisyCur<IN>& c, const NoisyTaps<IN>& tp,
                                                       int frame) {
     NoisyItem o;
     o.owner = c.owner;
     o.lin = pix(P, c.px, c.py);
-    o.n = c.nrm;
-    o.p = c.wp;
-    const f3 wp = c.wp, nrm = c.nrm, cur = c.cur;
+    const f3 wp = widen(c.wp), nrm = widen(c.nrm), cur = widen(c.cur);
+    o.n = nrm;
+    o.p = wp;
     uint8_t accept = 0;
     float alpha = 1.f;
     f3 prev{0.f, 0.f, 0.f};
@@ -365,11 +372,12 @@ __device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const No
         float total = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {  // bmfr.cl:374-419
-            const f3 d{tp.pp[i].x - wp.x, tp.pp[i].y - wp.y, tp.pp[i].z - wp.z};
-            const f3 dn{tp.pn[i].x - nrm.x, tp.pn[i].y - nrm.y, tp.pn[i].z - nrm.z};
+            const f3 pp = widen(tp.pp[i]), pn = widen(tp.pn[i]);
+            const f3 d{pp.x - wp.x, pp.y - wp.y, pp.z - wp.z};
+            const f3 dn{pn.x - nrm.x, pn.y - nrm.y, pn.z - nrm.z};
             if ((tp.inb & (1u << i)) && dot3(d, d) < P.position_limit_sq && dot3(dn, dn) < P.normal_limit_sq) {
                 accept |= (uint8_t)(1 << i);
-                sample_spp = sample_spp + tp.wts[i] * tp.sp[i];
+                sample_spp = sample_spp + tp.wts[i] * (float)tp.spu[i];
                 prev.x = prev.x + tp.wts[i] * tp.pc[i].x;
                 prev.y = prev.y + tp.wts[i] * tp.pc[i].y;
                 prev.z = prev.z + tp.wts[i] * tp.pc[i].z;
@@ -413,9 +421,9 @@ __device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const No
 
 template <bool FILT = false, class IN = float>
 __device__ __forceinline__ NoisyItem noisy_item_spec(const Params& P, const NoisyInputs& in, const Camera& cam,
-                                                     const NoisyCur& c, int frame,
+                                                     const NoisyCur<IN>& c, int frame,
                                                      const float* __restrict__ acc_prev = nullptr) {
-    return noisy_taps_finish<FILT>(P, c, noisy_taps_issue<FILT, IN>(P, in, cam, c, frame, acc_prev), frame);
+    return noisy_taps_finish<FILT, IN>(P, c, noisy_taps_issue<FILT, IN>(P, in, cam, c, frame, acc_prev), frame);
 }
 
 // One work-group's reprojection-reach report (tiled contexts): the lanes
