@@ -32,7 +32,7 @@ struct bmfr_ctx {
     hipStream_t side = nullptr;
     static constexpr int kSeqEvents = 4;
     hipEvent_t seq_k1[kSeqEvents] = {}, seq_k2[kSeqEvents] = {}, seq_start = nullptr;
-    double* noise_table = nullptr;  // kNoiseFrames consecutive frames' tables from noise_first
+    float* noise_table = nullptr;  // kNoiseFrames consecutive frames' tables from noise_first
     int noise_first = -1;
     unsigned long long* stamps = nullptr;  // diagnostic: BMFR_STAMPS=1 with libbmfr_diag.so
     int cur = 0;
@@ -345,7 +345,7 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
         e = hipMalloc(&c->stamps, (size_t)sz.blocks * 8 * sizeof(unsigned long long));
     if (e == hipSuccess)
         e = hipMalloc(&c->noise_table,
-                      (size_t)bmfr::kNoiseFrames * bmfr::kMaxFeatures * bmfr::kBlockPixels * sizeof(double));
+                      (size_t)bmfr::kNoiseFrames * bmfr::kMaxFeatures * bmfr::kBlockPixels * sizeof(float));
     if (e == hipSuccess && is_tiled(cfg)) {
         void* h = nullptr;
         e = hipMalloc(&c->reach_dev, sizeof(unsigned));
@@ -594,7 +594,7 @@ Params block_rect(Params P, int x0, int x1, int y0, int y1) {
 // stream s when f is outside the cached range.  Frames are ordered on their
 // streams by their state dependencies, so a batch is never rewritten under a
 // K1 that still reads it.
-hipError_t noise_for_frame(bmfr_ctx* c, const Params& P, hipStream_t s, int f, double** out) {
+hipError_t noise_for_frame(bmfr_ctx* c, const Params& P, hipStream_t s, int f, float** out) {
     const size_t per = (size_t)(P.buffers - 4) * bmfr::kBlockPixels;
     if (c->noise_first < 0 || f < c->noise_first || f >= c->noise_first + bmfr::kNoiseFrames) {
         const hipError_t e = bmfr::launch_noise_tables(P, s, f, bmfr::kNoiseFrames, c->noise_table);

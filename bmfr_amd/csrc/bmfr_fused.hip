@@ -136,7 +136,7 @@ __device__ __forceinline__ void block_reduce(float (&v)[K], K1Lds<B>& L, int t) 
 // One Householder column (bmfr.cl:549-655), compile-time column index.
 // ---------------------------------------------------------------------------
 template <int col, int B, class M>
-__device__ __forceinline__ void qr_column(M& A, K1Lds<B>& L, int t, const double* __restrict__ noise,
+__device__ __forceinline__ void qr_column(M& A, K1Lds<B>& L, int t, const float* __restrict__ noise,
                                           double noise2) {
     constexpr int RE = B - 2;
     constexpr int cl = col;  // col_limited (feature columns only)
@@ -167,7 +167,7 @@ __device__ __forceinline__ void qr_column(M& A, K1Lds<B>& L, int t, const double
                     for (int s = 0; s < kSubs; ++s) {
                         float v = A.get(fb, s);
                         if (fb < B - 3)
-                            v = (float)((double)v + noise[(fb - 1) * kBlockPixels + t + kLocal * s]);
+                            v = (float)((double)v + noise2 * (double)noise[(fb - 1) * kBlockPixels + t + kLocal * s]);
                         vals[k][s] = v;
                     }
                     float sum = row0 ? vals[k][0] * -31.f : vals[k][0];
@@ -249,7 +249,7 @@ __device__ __forceinline__ void qr_column(M& A, K1Lds<B>& L, int t, const double
 }
 
 template <int B, class M, int... C>
-__device__ __forceinline__ void qr_columns(M& A, K1Lds<B>& L, int t, const double* __restrict__ noise,
+__device__ __forceinline__ void qr_columns(M& A, K1Lds<B>& L, int t, const float* __restrict__ noise,
                                            double noise2, std::integer_sequence<int, C...>) {
     (qr_column<C, B>(A, L, t, noise, noise2), ...);
 }

@@ -169,22 +169,25 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
 // Step 0: column 0 is FEATURE_BUFFERS[0] = 1.f, so u = (1 - 32, 1, 1, ...),
 // |u|^2 = 1984 and u*x = x exactly (see k_fused's qr_column<0>).  Noise is
 // added to feature columns on this first load (bmfr.cl:625-627).
-// noise: the column's 1024 noise terms, or null (colour columns get none);
+// noise: the column's 1024 noise factors, or null (colour columns get none);
 // pre: this lane's 16 of them already loaded (the wave's first column).
-__device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const double* __restrict__ noise,
-                                               const double (&pre)[kSlots], bool use_pre) {
+// The table holds the float factors (rnd - 0.5f); the term is noise2 * factor
+// in double (bmfr.cl:173-182), formed here: 16 floats per lane -- one round
+// trip for the column's loads.
+__device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const float* __restrict__ noise,
+                                               const float (&pre)[kSlots], bool use_pre, double noise2) {
     float x[kSlots];
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
     if (use_pre) {  // wave-uniform
 #pragma unroll
-        for (int j = 0; j < kSlots; ++j) x[j] = (float)((double)x[j] + pre[j]);
+        for (int j = 0; j < kSlots; ++j) x[j] = (float)((double)x[j] + noise2 * (double)pre[j]);
     } else if (noise) {  // wave-uniform
+        float nz[kSlots];
 #pragma unroll
-        for (int j = 0; j < kSlots; ++j) {
-            x[j] = (float)((double)x[j] + noise[l + 64 * j]);
-            if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // 8 double loads in flight at a time
-        }
+        for (int j = 0; j < kSlots; ++j) nz[j] = noise[l + 64 * j];
+#pragma unroll
+        for (int j = 0; j < kSlots; ++j) x[j] = (float)((double)x[j] + noise2 * (double)nz[j]);
     }
     float p[4];
 #pragma unroll
@@ -306,12 +309,13 @@ struct WaveFit {
 
     template <int c>
     static __device__ __forceinline__ void step(h2 (&a)[NSL][8], Lds<B>& L, int W, int l,
-                                                const double* __restrict__ noise, const double (&pre)[kSlots]) {
+                                                const float* __restrict__ noise, const float (&pre)[kSlots],
+                                                double noise2) {
         constexpr int nxt = c + 1;  // the next pivot column, slot(nxt) of wave owner(nxt)
         const bool publish = nxt < NF && W == owner(nxt);
         if constexpr (c == 0) {
             if (publish) {  // column 1 of wave 0: its first column
-                update_column0(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre, true);
+                update_column0(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre, true, noise2);
                 publish_pivot<nxt, B>(a[slot(nxt)], L, l);
             }
             sfor<NSL>([&](auto K) {
@@ -319,7 +323,7 @@ struct WaveFit {
                 const int fb = 1 + W + 4 * k;
                 if (owns(W, fb) && !(publish && fb == nxt))
                     update_column0(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr, pre,
-                                   fb == first_column(W));
+                                   fb == first_column(W), noise2);
             });
         } else {
             if (1 + W + 4 * ((B - 2 - W) / 4) > c) {  // this wave's last column is past the pivot
@@ -357,22 +361,22 @@ struct WaveFit {
 
     template <int... C>
     static __device__ __forceinline__ void steps(h2 (&a)[NSL][8], Lds<B>& L, int W, int l,
-                                                 const double* __restrict__ noise, const double (&pre)[kSlots],
-                                                 std::integer_sequence<int, C...>) {
-        (step<C>(a, L, W, l, noise, pre), ...);
+                                                 const float* __restrict__ noise, const float (&pre)[kSlots],
+                                                 double noise2, std::integer_sequence<int, C...>) {
+        (step<C>(a, L, W, l, noise, pre, noise2), ...);
     }
 
     // Step 0's noise for the wave's first column, loaded while the last
     // items of phase 1 finish (it is every wave's first dependent load of the fit).
-    static __device__ __forceinline__ void prefetch_noise(int W, int l, const double* __restrict__ noise,
-                                                          double (&pre)[kSlots]) {
-        const double* src = noise + (first_column(W) - 1) * kBlockPixels + l;
+    static __device__ __forceinline__ void prefetch_noise(int W, int l, const float* __restrict__ noise,
+                                                          float (&pre)[kSlots]) {
+        const float* src = noise + (first_column(W) - 1) * kBlockPixels + l;
 #pragma unroll
         for (int j = 0; j < kSlots; ++j) pre[j] = src[64 * j];
     }
 
-    static __device__ __forceinline__ void run(Lds<B>& L, int W, int l, const double* __restrict__ noise,
-                                               const double (&pre)[kSlots]) {
+    static __device__ __forceinline__ void run(Lds<B>& L, int W, int l, const float* __restrict__ noise,
+                                               const float (&pre)[kSlots], double noise2) {
         h2 a[NSL][8];
         sfor<NSL>([&](auto K) {
             constexpr int k = decltype(K)::value;
@@ -427,7 +431,7 @@ struct WaveFit {
         });
         if (W == 0 && l < 3) L.R[l] = 32.f;  // R(0,0) = |column 0|
 
-        steps(a, L, W, l, noise, pre, std::make_integer_sequence<int, NF>{});
+        steps(a, L, W, l, noise, pre, noise2, std::make_integer_sequence<int, NF>{});
 
         // Right-hand side: rows 0..B-4 of the colour columns (bmfr.cl:596-600).
         sfor<NSL>([&](auto K) {
@@ -577,14 +581,14 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
         if (i < 3) cur = nxt;
     }
     report_reach(P, A.reach, over);
-    double pre[kSlots];
+    float pre[kSlots];
     WaveFit<NS, FS>::prefetch_noise(w, l, A.noise, pre);
     k1_barrier();  // matrix in LDS; phase 1's global stores drain in the background
     BMFR_STAMP(1);
     BMFR_STAMP(2);  // scaling runs inside the per-wave fit
 
     // ---- fit: min/max scaling, Householder QR, right-hand side ----
-    WaveFit<NS, FS>::run(L, w, l, A.noise, pre);
+    WaveFit<NS, FS>::run(L, w, l, A.noise, pre, P.noise2);
     // Phase 3's loads (normal and position of the four items, bmfr.cl:725-729)
     // go out now: they land while wave 0 back-substitutes and the others wait.
     int l3 = l;  // opaque copy: recompute phase-1 addresses instead of keeping them live across the fit

@@ -167,16 +167,17 @@ hipError_t launch_halo_copy(const HaloArgs& a, hipStream_t st, void* buf, int un
 // for fb = 1..B-4; the kernel forms NOISE_AMOUNT*2.f*that in double as upstream.
 // Tables of `frames` consecutive frames from `first` are made in one launch
 // (one per kNoiseFrames frames), frame first + k at table + k * per_frame.
-__global__ __launch_bounds__(256) void k_noise_table(int first, int frames, int buffers, double noise2,
-                                                     double* __restrict__ table) {
+__global__ __launch_bounds__(256) void k_noise_table(int first, int frames, int buffers, float* __restrict__ table) {
     const int per_frame = (buffers - 4) * kBlockPixels;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= frames * per_frame) return;
     const int frame = first + i / per_frame, j = i % per_frame;
     const int fb = 1 + j / kBlockPixels, r = j % kBlockPixels;
-    // add_random's addend (bmfr.cl:173-182) for row r of feature fb: the same
-    // for every block, so computed once per frame.
-    table[i] = noise2 * (double)(hash_random((uint32_t)(r + fb * kBlockPixels + frame * buffers * kBlockPixels)) - 0.5f);
+    // add_random's addend (bmfr.cl:173-182) for row r of feature fb is
+    // NOISE_AMOUNT * 2 (double) times this float: the same for every block, so
+    // computed once per frame; the fitters form the double product (exactly
+    // upstream's) where they add it -- half the bytes of storing the double.
+    table[i] = hash_random((uint32_t)(r + fb * kBlockPixels + frame * buffers * kBlockPixels)) - 0.5f;
 }
 
 // ---------------------------------------------------------------- launch --
@@ -250,10 +251,9 @@ hipError_t launch_taa(const Params& P, hipStream_t st, const float2* prev_pixel,
     return hipGetLastError();
 }
 
-hipError_t launch_noise_tables(const Params& P, hipStream_t st, int first, int frames, double* table) {
+hipError_t launch_noise_tables(const Params& P, hipStream_t st, int first, int frames, float* table) {
     const int n = frames * (P.buffers - 4) * kBlockPixels;
-    hipLaunchKernelGGL(k_noise_table, dim3((n + 255) / 256), dim3(256), 0, st, first, frames, P.buffers, P.noise2,
-                       table);
+    hipLaunchKernelGGL(k_noise_table, dim3((n + 255) / 256), dim3(256), 0, st, first, frames, P.buffers, table);
     return hipGetLastError();
 }
 

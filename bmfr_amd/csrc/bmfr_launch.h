@@ -36,7 +36,7 @@ struct FusedArgs {
     float* acc_out;
     float* tone_out;
     float* result_out;
-    double* noise_table;  // (B-4) * 1024 noise terms NOISE_AMOUNT*2*(rnd-0.5) in double, context-owned
+    float* noise_table;   // (B-4) * 1024 noise factors rnd-0.5f (the term is NOISE_AMOUNT*2 * that, in double), context-owned
     unsigned* reach;      // tiled contexts: max overshoot (px) of reprojection taps past the valid state
     unsigned* reach_host; // tiled contexts: page-locked report of it (see TaaArgs)
     unsigned long long* stamps;  // diagnostic build: 8 timestamps per block, or null
@@ -54,7 +54,7 @@ struct K1Args {
     uint8_t* spp_out;
     float2* prev_pixel_out;
     float* acc_out;
-    const double* noise;
+    const float* noise;
     unsigned* reach;
     unsigned long long* stamps;
     unsigned* done;
@@ -99,7 +99,7 @@ hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& 
 hipError_t launch_noise_table(const Params& P, hipStream_t st, const FusedArgs& A);
 // Noise tables of frames first .. first+frames-1, back to back from `table`.
 constexpr int kNoiseFrames = 64;
-hipError_t launch_noise_tables(const Params& P, hipStream_t st, int first, int frames, double* table);
+hipError_t launch_noise_tables(const Params& P, hipStream_t st, int first, int frames, float* table);
 hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedArgs& A);
 // Sequence kernel (bmfr_process_sequence): K1 of a frame (A, or none) and K2
 // of the frame before it (A2, or none) in one launch.
