@@ -38,6 +38,7 @@ constexpr int kThreads = 256;
 constexpr int kSlots = 16;    // rows per lane per column (row = lane + 64 j)
 constexpr int kStagger = 24000;  // cycles between first-round work-group groups (k1_stagger)
 constexpr int kUStride = 20;     // floats per lane in a u buffer: 16 + 4 (conflict-free 16-byte reads)
+constexpr int kPre = 2;          // step-0 noise columns per wave prefetched in phase 1
 
 // Householder vectors in flight: the fit's waves wait for each published
 // pivot through an LDS flag instead of a barrier per column, so a buffer is
@@ -306,24 +307,25 @@ struct WaveFit {
 
     // The first column a wave updates at step 0: a feature column for every wave.
     static __device__ __forceinline__ int first_column(int W) { return 1 + W; }
+    static_assert(5 + 3 < NF, "the first two columns of every wave are feature columns");
 
     template <int c>
     static __device__ __forceinline__ void step(h2 (&a)[NSL][8], Lds<B>& L, int W, int l,
-                                                const float* __restrict__ noise, const float (&pre)[kSlots],
+                                                const float* __restrict__ noise, const float (&pre)[kPre][kSlots],
                                                 double noise2) {
         constexpr int nxt = c + 1;  // the next pivot column, slot(nxt) of wave owner(nxt)
         const bool publish = nxt < NF && W == owner(nxt);
         if constexpr (c == 0) {
             if (publish) {  // column 1 of wave 0: its first column
-                update_column0(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre, true, noise2);
+                update_column0(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre[0], true, noise2);
                 publish_pivot<nxt, B>(a[slot(nxt)], L, l);
             }
             sfor<NSL>([&](auto K) {
                 constexpr int k = decltype(K)::value;
                 const int fb = 1 + W + 4 * k;
-                if (owns(W, fb) && !(publish && fb == nxt))
-                    update_column0(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr, pre,
-                                   fb == first_column(W), noise2);
+                if (owns(W, fb) && !(publish && fb == nxt))  // slots < kPre: feature columns, prefetched
+                    update_column0(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr,
+                                   pre[k < kPre ? k : 0], k < kPre, noise2);
             });
         } else {
             if (1 + W + 4 * ((B - 2 - W) / 4) > c) {  // this wave's last column is past the pivot
@@ -361,22 +363,27 @@ struct WaveFit {
 
     template <int... C>
     static __device__ __forceinline__ void steps(h2 (&a)[NSL][8], Lds<B>& L, int W, int l,
-                                                 const float* __restrict__ noise, const float (&pre)[kSlots],
+                                                 const float* __restrict__ noise, const float (&pre)[kPre][kSlots],
                                                  double noise2, std::integer_sequence<int, C...>) {
         (step<C>(a, L, W, l, noise, pre, noise2), ...);
     }
 
-    // Step 0's noise for the wave's first column, loaded while the last
-    // items of phase 1 finish (it is every wave's first dependent load of the fit).
+    // Step 0's noise for the wave's first kPre columns (1 + W, 5 + W: feature
+    // columns for every wave), loaded while the last items of phase 1 finish
+    // (the fit's first dependent loads); with B = 13 only wave 0 has a third
+    // noisy column, loaded in step 0.
     static __device__ __forceinline__ void prefetch_noise(int W, int l, const float* __restrict__ noise,
-                                                          float (&pre)[kSlots]) {
-        const float* src = noise + (first_column(W) - 1) * kBlockPixels + l;
+                                                          float (&pre)[kPre][kSlots]) {
 #pragma unroll
-        for (int j = 0; j < kSlots; ++j) pre[j] = src[64 * j];
+        for (int k = 0; k < kPre; ++k) {
+            const float* src = noise + (first_column(W) + 4 * k - 1) * kBlockPixels + l;
+#pragma unroll
+            for (int j = 0; j < kSlots; ++j) pre[k][j] = src[64 * j];
+        }
     }
 
     static __device__ __forceinline__ void run(Lds<B>& L, int W, int l, const float* __restrict__ noise,
-                                               const float (&pre)[kSlots], double noise2) {
+                                               const float (&pre)[kPre][kSlots], double noise2) {
         h2 a[NSL][8];
         sfor<NSL>([&](auto K) {
             constexpr int k = decltype(K)::value;
@@ -581,7 +588,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
         if (i < 3) cur = nxt;
     }
     report_reach(P, A.reach, over);
-    float pre[kSlots];
+    float pre[kPre][kSlots];
     WaveFit<NS, FS>::prefetch_noise(w, l, A.noise, pre);
     k1_barrier();  // matrix in LDS; phase 1's global stores drain in the background
     BMFR_STAMP(1);
