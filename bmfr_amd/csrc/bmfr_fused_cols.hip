@@ -602,20 +602,26 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     asm volatile("" : "+v"(l3));
     const int2 off = kBlockOffsets[frame & 15];
     uint32_t lin[4];
-    f3 nrm[4], wp[4];
+    In3<IN> nrm_r[4], wp_r[4];  // as loaded: widened after the back substitution
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int px = bx * kEdge + (l3 & (kEdge - 1)) - kEdge / 2 + off.x;
         const int py = by * kEdge + (l3 >> 5) + 8 * w + 2 * i - kEdge / 2 + off.y;
         lin[i] = pix(P, (ibits & (1u << i)) ? px : P.ox, (ibits & (1u << i)) ? py : P.oy);  // margins: a valid pixel, skipped below
-        nrm[i] = ld3in<IN>(A.in.n_cur, lin[i]);
-        wp[i] = ld3in<IN>(A.in.p_cur, lin[i]);
+        nrm_r[i] = ld3raw<IN>(A.in.n_cur, lin[i]);
+        wp_r[i] = ld3raw<IN>(A.in.p_cur, lin[i]);
     }
     k1_barrier();  // R complete (LDS); with LDS-only barriers the loads above stay in flight
     BMFR_STAMP(3);
     back_substitute_regs<B>(L, t);
     k1_barrier();  // weights complete
     BMFR_STAMP(4);
+    f3 nrm[4], wp[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        nrm[i] = widen(nrm_r[i]);
+        wp[i] = widen(wp_r[i]);
+    }
 
     // ---- weighted_sum (bmfr.cl:717-750) + temporal blend (bmfr.cl:778-849) ----
     // Features outer, items inner: each weight / min-max is live for one
