@@ -36,7 +36,6 @@ namespace cols {
 
 constexpr int kThreads = 256;
 constexpr int kSlots = 16;    // rows per lane per column (row = lane + 64 j)
-constexpr int kStagger = 24000;  // cycles between first-round work-group groups (k1_stagger)
 constexpr int kUStride = 20;     // floats per lane in a u buffer: 16 + 4 (conflict-free 16-byte reads)
 constexpr int kPre = 2;          // step-0 noise columns per wave prefetched in phase 1
 
@@ -691,21 +690,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     }
 }
 
-// First round of work-groups: start the k-th group of 256 k * kStagger
-// cycles late, so the four work-groups sharing a CU do not run their
-// memory-bound phase 1 and VALU-bound fit in lockstep (large launches only,
-// not a tile's border ring).
-__device__ __forceinline__ void k1_stagger(int b, int n) {
-    if (b < 4 * 256 && n >= 8 * 256) {
-        const int k = ((b >> 8) & 3) * (kStagger / 8000);
-        for (int s = 0; s < k; ++s) __builtin_amdgcn_s_sleep(125);
-    }
-}
-
 template <int NS, int FS, class IN>
 __global__ __launch_bounds__(kThreads, kColsWaves) void k_fused_cols(Params P, K1Args A) {
     __shared__ Lds<NS + FS + 3> L;
-    k1_stagger(blockIdx.x, gridDim.x);
     k1_cols_body<NS, FS, IN>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
 }
 
@@ -737,7 +724,6 @@ __global__ __launch_bounds__(kThreads, 4) void k_fused_cols_taa(Params P, K1Args
     } U;
     const int b = blockIdx.x;
     if (b < nk1) {
-        k1_stagger(b, nk1);
         k1_cols_body<NS, FS, IN, SAME>(P, A, U.k1, xcd_swizzle(b, nk1));
     } else if (b >= nk1p) {
         const int gx = (P2.tx1 - P2.tx0 + 63) / 64, n2 = (int)gridDim.x - nk1p;
