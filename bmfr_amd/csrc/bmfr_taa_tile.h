@@ -87,7 +87,8 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
         if constexpr (COH) pf[k] = ld2_coh(c_pp, i);
         else pf[k] = ld_px(T.prev_pixel, i);
     }
-    f3 v[KN + 1], al[KN + 1];
+    f3 v[KN + 1];
+    In3<IN> al[KN + 1];  // albedo as loaded, widened in the tone map (after the tap loads are out)
     int hx = 0, hy = 0;  // this thread's ring pixel (t < RING), in tile + halo coordinates
     if (t < 2 * HW) {
         hx = t % HW;
@@ -106,7 +107,7 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
         const uint32_t lin = pix(P, clamp_rx(P, x0 - 1 + lx), clamp_ry(P, y0 - 1 + ly));
         if constexpr (COH) v[k] = ld3_coh(c_src, lin);
         else v[k] = ld3(T.src, lin);
-        al[k] = ld3in<IN>(T.albedo, lin);
+        al[k] = ld3raw<IN>(T.albedo, lin);
     }
     // Previous-frame taps before the tone map: their latency hides under it.
     f3 taps[KN][4];
@@ -117,7 +118,7 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
     for (int k = 0; k <= KN; ++k) {
         if (k == KN && t >= RING) break;
         const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + 4 * k + 1 : hy;
-        v[k] = tone_map(P, al[k], v[k], sE, sRP);
+        v[k] = tone_map(P, widen(al[k]), v[k], sE, sRP);
         const f3 yc = rgb_to_ycocg(v[k]);
         Y[ly * HW + lx] = make_float4(yc.x, yc.y, yc.z, 0.f);
     }
