@@ -28,8 +28,10 @@ POSITION_X3, POSITION_Y3, POSITION_Z3 = 10, 11, 12
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "unsupported configuration",
           3: "out of device memory", 4: "HIP runtime error", 5: "no HIP device",
-          6: "reprojection reached past the tile halo"}
+          6: "reprojection reached past the tile halo",
+          7: "a kernel's bounded wait for another work-group gave up"}
 HALO_EXCEEDED = 6
+SYNC_TIMEOUT = 7
 
 
 class BmfrError(RuntimeError):
@@ -108,12 +110,14 @@ SIGNATURES = {
     "bmfr_process_frame_border": (_I, [_P, _P, C.POINTER(FrameInputs), _F16, _F2, _I]),
     "bmfr_output": (_P, [_P]),
     "bmfr_halo_status": (_I, [_P, C.POINTER(C.c_uint)]),
+    "bmfr_frame_status": (_I, [_P]),
     "bmfr_state": (_I, [_P, _I, C.POINTER(StateView)]),
     "bmfr_set_profiling": (_I, [_P, _I, _I]),
     "bmfr_set_profiling_stride": (_I, [_P, _I]),
     "bmfr_get_profile": (_I, [_P, C.POINTER(FrameProfile), _I, C.POINTER(_I)]),
     "bmfr_synth_camera": (None, [_I, _I, _I, _F16, _F2]),
     "bmfr_debug_stamps": (_I, [_P, _P, C.c_size_t]),  # include/bmfr_debug.h
+    "bmfr_debug_sync": (_I, [_P, _I, _I]),  # include/bmfr_debug.h
     "bmfr_synth_frame_host": (_I, [_I, _I, _I, C.c_uint32, _P, _P, _P, _P, _P]),
     "bmfr_synth_frame_device": (_I, [_I, _I, _I, C.c_uint32, _P, _P, _P, _P, _P, _P]),
     "bmfr_synth_region_device": (_I, [_I, _I, _I, _I, _I, _I, _I, C.c_uint32, _P, _P, _P, _P, _P, _P]),
@@ -130,6 +134,8 @@ def load() -> C.CDLL:
             raise ImportError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
         lib = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if _variant and not hasattr(lib, name):
+                continue  # an A/B build of older sources may predate a symbol
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

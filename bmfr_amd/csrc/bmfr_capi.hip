@@ -45,7 +45,12 @@ struct bmfr_ctx {
     // max over frames since frame 0) and stamps reach_host[1] = frame + 1.
     unsigned* reach_dev = nullptr;
     volatile unsigned* reach_host = nullptr;
-    hipEvent_t reach_event = nullptr;  // after the last frame's K2
+    // Every context: page-locked words the kernels set when a bounded wait
+    // gave up ([kSyncPivot], [kSyncTile]: frame + 1), and an event after the
+    // last enqueued frame (bmfr_frame_status / bmfr_halo_status wait on it).
+    volatile unsigned* sync_host = nullptr;
+    hipEvent_t frame_event = nullptr;
+    bool frame_enqueued = false;
     // One-launch frames (untiled canonical half-tmp_data path): per K1 block
     // the epoch of the last launch that completed it; epoch counts launches.
     unsigned* done = nullptr;
@@ -173,6 +178,8 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     P.vx1 = P.ox + P.stride;
     P.vy1 = P.oy + P.rows;
     P.wx0 = P.vx0, P.wy0 = P.vy0, P.wx1 = P.vx1, P.wy1 = P.vy1;
+    P.max_polls = bmfr::kDefaultMaxPolls;
+    P.debug_delay = 0;
     return P;
 }
 
@@ -307,6 +314,7 @@ const char* bmfr_status_string(bmfr_status s) {
         case BMFR_ERROR_HIP: return "HIP runtime error";
         case BMFR_ERROR_NO_DEVICE: return "no HIP device";
         case BMFR_ERROR_HALO_EXCEEDED: return "reprojection reached past the tile halo";
+        case BMFR_ERROR_SYNC_TIMEOUT: return "a kernel's bounded wait for another work-group gave up";
     }
     return "unknown status";
 }
@@ -346,6 +354,15 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
     if (e == hipSuccess)
         e = hipMalloc(&c->noise_table,
                       (size_t)bmfr::kNoiseFrames * bmfr::kMaxFeatures * bmfr::kBlockPixels * sizeof(float));
+    if (e == hipSuccess) {
+        void* h = nullptr;
+        e = hipHostMalloc(&h, 2 * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) {
+            c->sync_host = static_cast<volatile unsigned*>(h);
+            c->sync_host[0] = c->sync_host[1] = 0;
+            e = hipEventCreateWithFlags(&c->frame_event, hipEventDisableTiming);
+        }
+    }
     if (e == hipSuccess && is_tiled(cfg)) {
         void* h = nullptr;
         e = hipMalloc(&c->reach_dev, sizeof(unsigned));
@@ -354,7 +371,6 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
         if (e == hipSuccess) {
             c->reach_host = static_cast<volatile unsigned*>(h);
             c->reach_host[0] = c->reach_host[1] = 0;
-            e = hipEventCreateWithFlags(&c->reach_event, hipEventDisableTiming);
         }
     }
     if (e == hipSuccess && bmfr::frame_fused_supported(c->P)) {
@@ -374,8 +390,10 @@ bmfr_status bmfr_destroy(bmfr_ctx* c) {
     DeviceGuard guard(c->device);
     (void)hipFree(c->reach_dev);
     (void)hipFree(c->done);
+    if (c->frame_event) (void)hipEventSynchronize(c->frame_event);  // no kernel still writes the host words
     if (c->reach_host) (void)hipHostFree(const_cast<unsigned*>(c->reach_host));
-    if (c->reach_event) (void)hipEventDestroy(c->reach_event);
+    if (c->sync_host) (void)hipHostFree(const_cast<unsigned*>(c->sync_host));
+    if (c->frame_event) (void)hipEventDestroy(c->frame_event);
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(c->noisy_acc[i]);
         (void)hipFree(c->spp[i]);
@@ -527,20 +545,40 @@ bmfr::FusedArgs frame_args(const bmfr_ctx* c, const bmfr_frame_inputs* in, const
     A.stamps = c->stamps;
     A.done = nullptr;  // set per launch (one_launch_args)
     A.epoch = 0;
+    A.sync_err = const_cast<unsigned*>(c->sync_host);
     return A;
 }
 
-// Tiled contexts: BMFR_ERROR_HALO_EXCEEDED once a completed frame reported
-// reprojection taps past the exchanged state (sticky until frame 0).
-bmfr_status reach_check(bmfr_ctx* c, int frame_number) {
-    if (!c->reach_host) return BMFR_OK;
-    if (frame_number == 0 && c->reach_host[0] > 0) {  // a new sequence: clear the report
-        const bmfr_status st = hip_status(hipEventSynchronize(c->reach_event));
-        if (st != BMFR_OK) return st;
-        c->reach_host[0] = 0;
+// The sticky reports of completed frames, as the host sees them now (no wait).
+bmfr_status reported(const bmfr_ctx* c) {
+    if (c->sync_host[bmfr::kSyncPivot] || c->sync_host[bmfr::kSyncTile]) return BMFR_ERROR_SYNC_TIMEOUT;
+    if (c->reach_host && c->reach_host[0] > 0) return BMFR_ERROR_HALO_EXCEEDED;
+    return BMFR_OK;
+}
+
+// Before a frame is enqueued: BMFR_ERROR_SYNC_TIMEOUT once a completed frame
+// reported an exhausted wait, and (tiled contexts) BMFR_ERROR_HALO_EXCEEDED
+// once one reported reprojection taps past the exchanged state -- both sticky
+// until frame 0 starts a new sequence.  Frame 0 first waits for every frame
+// already enqueued (a frame still in flight could raise a report after it was
+// cleared), then clears them.
+bmfr_status status_check(bmfr_ctx* c, int frame_number) {
+    if (frame_number == 0) {
+        if (c->frame_enqueued) {
+            const bmfr_status st = hip_status(hipEventSynchronize(c->frame_event));
+            if (st != BMFR_OK) return st;
+        }
+        c->sync_host[0] = c->sync_host[1] = 0;
+        if (c->reach_host) c->reach_host[0] = 0;
         return BMFR_OK;
     }
-    return c->reach_host[0] > 0 ? BMFR_ERROR_HALO_EXCEEDED : BMFR_OK;
+    return reported(c);
+}
+
+// After a frame's last kernel: the event bmfr_frame_status waits on.
+void frame_enqueued(bmfr_ctx* c, hipStream_t s) {
+    (void)hipEventRecord(c->frame_event, s);
+    c->frame_enqueued = true;
 }
 
 // Blocks of frame `frame`'s K1 launch (frame_params) whose reads of the
@@ -614,7 +652,7 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
     if (part == 1 && c->pending_frame != frame_number) return BMFR_ERROR_INVALID_ARGUMENT;
     if (part != 1 && c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
     DeviceGuard guard(c->device);
-    if (part != 1 && (st = reach_check(c, frame_number)) != BMFR_OK) return st;
+    if (part != 1 && (st = status_check(c, frame_number)) != BMFR_OK) return st;
     const hipStream_t s = as_stream(stream);
     const int cur = c->has_frame ? 1 - c->cur : 0;  // swap, bmfr.cpp:482-484
     bmfr::FusedArgs A = frame_args(c, in, m, off, frame_number, cur);
@@ -637,7 +675,7 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
         if (bmfr::fused_supported(P) && (st = hip_status(noise_for_frame(c, P, s, frame_number, &A.noise_table))))
             return st;
         if (c->done && !ev) {  // one launch: the next epoch (never 0; flags reset on wrap)
-            if (++c->epoch == 0) {
+            if (++c->epoch == bmfr::kDoneTimeout) {  // the flag's top bit carries a timeout
                 if ((st = hip_status(hipMemsetAsync(c->done, 0, done_bytes(c), s))))
                     return st;
                 c->epoch = 1;
@@ -678,7 +716,7 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
         c->pending_prof_slot = -1;
     }
     if (ev) (void)hipEventRecord(ev[2], s);
-    if (c->reach_event) (void)hipEventRecord(c->reach_event, s);
+    frame_enqueued(c, s);
     c->cur = cur;
     c->has_frame = true;
     return BMFR_OK;
@@ -700,10 +738,11 @@ bmfr_status bmfr_process_sequence(bmfr_ctx* c, void* stream, int count, const bm
     if (c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
     if (is_tiled(&c->cfg)) return BMFR_ERROR_UNSUPPORTED;  // tiles exchange a halo between frames
     DeviceGuard guard(c->device);
+    bmfr_status st = status_check(c, first_frame);
+    if (st != BMFR_OK) return st;
     const hipStream_t s = as_stream(stream);
     const size_t out_bytes = c->sizes.region_bytes;
     const bool pipelined = bmfr::fused_supported(c->P);
-    bmfr_status st;
     if (!pipelined) {  // frame after frame on `stream`
         for (int i = 0; i < count; ++i) {
             st = bmfr_process_frame(c, stream, &in[i], prev_frame_camera_matrices + 16 * i, pixel_offsets + 2 * i,
@@ -766,6 +805,7 @@ bmfr_status bmfr_process_sequence(bmfr_ctx* c, void* stream, int count, const bm
                 c->has_frame = true;
             }
         }
+        frame_enqueued(c, s);
         return BMFR_OK;
     }
     if (!c->side) {
@@ -814,7 +854,10 @@ bmfr_status bmfr_process_sequence(bmfr_ctx* c, void* stream, int count, const bm
         c->cur = cur;
         c->has_frame = true;
     }
-    return hip_status(hipStreamWaitEvent(s, c->seq_k2[(count - 1) % bmfr_ctx::kSeqEvents], 0));
+    if ((st = hip_status(hipStreamWaitEvent(s, c->seq_k2[(count - 1) % bmfr_ctx::kSeqEvents], 0))) != BMFR_OK)
+        return st;
+    frame_enqueued(c, s);
+    return BMFR_OK;
 }
 
 bmfr_status bmfr_process_frame_interior(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
@@ -937,13 +980,25 @@ bmfr_status bmfr_get_profile(bmfr_ctx* c, bmfr_frame_profile* out, int max_frame
 bmfr_status bmfr_halo_status(bmfr_ctx* c, unsigned* overshoot) {
     if (!c) return BMFR_ERROR_INVALID_ARGUMENT;
     if (overshoot) *overshoot = 0;
-    if (!c->reach_host) return BMFR_OK;  // untiled: the whole image is valid state
     DeviceGuard guard(c->device);
-    const bmfr_status st = hip_status(hipEventSynchronize(c->reach_event));
-    if (st != BMFR_OK) return st;
-    const unsigned v = c->reach_host[0];
-    if (overshoot) *overshoot = v;
-    return v > 0 ? BMFR_ERROR_HALO_EXCEEDED : BMFR_OK;
+    if (c->frame_enqueued) {
+        const bmfr_status st = hip_status(hipEventSynchronize(c->frame_event));
+        if (st != BMFR_OK) return st;
+    }
+    if (c->reach_host && overshoot) *overshoot = c->reach_host[0];  // untiled: the whole image is valid state
+    return reported(c);
+}
+
+bmfr_status bmfr_frame_status(bmfr_ctx* c) {
+    if (!c) return BMFR_ERROR_INVALID_ARGUMENT;
+    return bmfr_halo_status(c, nullptr);
+}
+
+bmfr_status bmfr_debug_sync(bmfr_ctx* c, int max_polls, int k1_delay) {
+    if (!c || k1_delay < 0 || c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
+    c->P.max_polls = max_polls < 0 ? bmfr::kDefaultMaxPolls : max_polls;
+    c->P.debug_delay = k1_delay;
+    return BMFR_OK;
 }
 
 bmfr_status bmfr_debug_stamps(const bmfr_ctx* c, unsigned long long* host, size_t count) {

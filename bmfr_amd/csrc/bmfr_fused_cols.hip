@@ -53,6 +53,9 @@ struct Lds {
     float piv[kUBufs][2];               // |u|^2 and RN(1/|u|^2) of the published vector
     int pub;                            // highest published pivot column
     int prog[4];                        // per wave: the last step it has applied
+    int timeout;                        // a flag wait of this block gave up (reported once, at the end)
+    int max_polls;                      // Params::max_polls (kept here: read only once a flag is not ready)
+    int delay;                          // Params::debug_delay (diagnostics, read at the block's end)
     float R[(B - 2) * (B - 2) * 3];     // R[x][y][ch], x = column (as k_fused)
     float weights[(B - 3) * 3];
     float mm[3 * (B - 3)];              // per scaled feature: min, max, 1/(max-min)
@@ -223,18 +226,30 @@ __device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const float* _
 // LDS flags of the fit: wave-uniform polls with a short sleep.  A publisher
 // waits for lgkmcnt(0) before raising the flag, so the data it wrote is in
 // LDS before any wave can see the flag.
-// The polls are bounded (~2^20 sleeps): a scheduling bug would then give
-// wrong results instead of a wave that never finishes.
-constexpr int kMaxPolls = 1 << 20;
-__device__ __forceinline__ void wait_pub(const int* pub, int c) {
-    for (int k = 0; k < kMaxPolls && __hip_atomic_load(pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c; ++k)
+// The polls are bounded (mp = Params::max_polls sleeps): a wave that gives up
+// marks the block (*timeout), the block reports BMFR_ERROR_SYNC_TIMEOUT
+// (report_sync_timeout) and runs to its end -- a scheduling bug gives a
+// reported error, never a wave that never finishes nor silently wrong pixels.
+template <int B>
+__device__ __forceinline__ void wait_flag(Lds<B>& L, const int* flag, int c) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= c) return;
+    const int mp = L.max_polls;
+    for (int k = 0;; ++k) {
+        if (k >= mp) {  // wave-uniform
+            L.timeout = 1;
+            return;
+        }
         __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= c) return;
+    }
 }
-__device__ __forceinline__ void wait_all_progress(const int* prog, int c) {
-    for (int w = 0; w < 4; ++w)
-        for (int k = 0;
-             k < kMaxPolls && __hip_atomic_load(&prog[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c; ++k)
-            __builtin_amdgcn_s_sleep(1);
+template <int B>
+__device__ __forceinline__ void wait_pub(Lds<B>& L, int c) {
+    wait_flag(L, &L.pub, c);
+}
+template <int B>
+__device__ __forceinline__ void wait_all_progress(Lds<B>& L, int c) {
+    for (int w = 0; w < 4; ++w) wait_flag(L, &L.prog[w], c);
 }
 
 // The owner of pivot column c (>= 1), once steps 0..c-1 are applied to it:
@@ -266,7 +281,7 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B>& L, int l
     const float ulen2 = sumsq + ucl2 * ucl2;
     if (l == c) x[0] = ucl2;
     constexpr int buf = c % kUBufs;
-    if constexpr (c >= kUBufs) wait_all_progress(L.prog, c - kUBufs);  // readers of u_{c-3} done
+    if constexpr (c >= kUBufs) wait_all_progress(L, c - kUBufs);  // readers of u_{c-3} done
     float4* dst = reinterpret_cast<float4*>(&L.u[buf][l * kUStride]);
 #pragma unroll
     for (int q = 0; q < 4; ++q) dst[q] = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
@@ -328,7 +343,7 @@ struct WaveFit {
             });
         } else {
             if (1 + W + 4 * ((B - 2 - W) / 4) > c) {  // this wave's last column is past the pivot
-                wait_pub(&L.pub, c);
+                wait_pub(L, c);
                 float u[kSlots];
                 const float4* src = reinterpret_cast<const float4*>(&L.u[c % kUBufs][l * kUStride]);
 #pragma unroll
@@ -382,7 +397,7 @@ struct WaveFit {
     }
 
     static __device__ __forceinline__ void run(Lds<B>& L, int W, int l, const float* __restrict__ noise,
-                                               const float (&pre)[kPre][kSlots], double noise2) {
+                                               const float (&pre)[kPre][kSlots], double noise2, int mp) {
         h2 a[NSL][8];
         sfor<NSL>([&](auto K) {
             constexpr int k = decltype(K)::value;
@@ -395,8 +410,10 @@ struct WaveFit {
                 for (int i = 0; i < 8; ++i) a[k][i] = __builtin_bit_cast(h2, src[i ^ q]);
             }
         });
-        if (W == 0 && l < 5) {  // read only after the barrier below
+        if (W == 0 && l < 7) {  // read only after the barrier below
             if (l == 0) L.pub = 0;
+            else if (l == 5) L.timeout = 0;
+            else if (l == 6) L.max_polls = mp;
             else L.prog[l - 1] = -1;
         }
         k1_barrier();  // the u buffers alias M
@@ -594,7 +611,8 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     BMFR_STAMP(2);  // scaling runs inside the per-wave fit
 
     // ---- fit: min/max scaling, Householder QR, right-hand side ----
-    WaveFit<NS, FS>::run(L, w, l, A.noise, pre, P.noise2);
+    if (t == 0) L.delay = P.debug_delay;  // read after the fit's barriers
+    WaveFit<NS, FS>::run(L, w, l, A.noise, pre, P.noise2, P.max_polls);
     // Phase 3's loads (normal and position of the four items, bmfr.cl:725-729)
     // go out now: they land while wave 0 back-substitutes and the others wait.
     int l3 = l;  // opaque copy: recompute phase-1 addresses instead of keeping them live across the fit
@@ -614,6 +632,11 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     BMFR_STAMP(3);
     back_substitute_regs<B>(L, t);
     k1_barrier();  // weights complete
+    // An exhausted pivot wait: reported here, or (one-launch frame) carried by
+    // the block's completion flag to the tiles that read it (fewer values
+    // live across the kernel).
+    if constexpr (!COH)
+        if (t == 0 && L.timeout) report_sync_timeout(A.sync_err, kSyncPivot, frame);
     BMFR_STAMP(4);
     f3 nrm[4], wp[4];
 #pragma unroll
@@ -684,9 +707,14 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 #endif
 #undef BMFR_STAMP
     if constexpr (COH) {
+        const int delay = L.delay;
+        if (delay > 0 && g % kDelayStride == kDelayPhase)  // diagnostics: tiles really wait
+            for (int k = 0; k < delay; ++k) __builtin_amdgcn_s_sleep(127);
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's stores are performed
         lds_barrier();                       // ... and every wave's
-        if (t == 0) __hip_atomic_store(&A.done[g], A.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0)
+            __hip_atomic_store(&A.done[g], A.epoch | (L.timeout ? kDoneTimeout : 0u), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

@@ -42,6 +42,7 @@ struct FusedArgs {
     unsigned long long* stamps;  // diagnostic build: 8 timestamps per block, or null
     unsigned* done;       // one-launch frame: per K1 block, the epoch of the launch that completed it
     unsigned epoch;       // this launch's epoch (context-wide launch counter, never 0)
+    unsigned* sync_err;   // page-locked report of an exhausted wait (kSyncPivot / kSyncTile), or null
 };
 
 // Kernel arguments of the fused K1 (canonical feature lists).
@@ -59,14 +60,15 @@ struct K1Args {
     unsigned long long* stamps;
     unsigned* done;
     unsigned epoch;
+    unsigned* sync_err;
 };
 inline K1Args k1_args(const FusedArgs& A) {
     return K1Args{A.in,      A.cam,         A.frame, A.acc_prev, A.noisy_out, A.spp_out, A.prev_pixel_out,
-                  A.acc_out, A.noise_table, A.reach, A.stamps,   A.done,      A.epoch};
+                  A.acc_out, A.noise_table, A.reach, A.stamps,   A.done,      A.epoch,   A.sync_err};
 }
 inline TaaArgs taa_args(const FusedArgs& A) {
     return TaaArgs{A.acc_out, A.albedo, A.prev_pixel_out, A.result_out, A.result_prev, A.frame, A.reach,
-                   A.reach_host, A.done, A.epoch};
+                   A.reach_host, A.done, A.epoch, A.sync_err};
 }
 
 bool fitter_supported(int not_scaled, int scaled);

@@ -60,7 +60,20 @@ struct Params {
     int check_reach;
     int vx0, vy0, vx1, vy1;
     int wx0, wy0, wx1, wy1;
+    // Bounded waits of the fused kernels (K1's LDS pivot flags, the
+    // one-launch frame's K1 completion flags): a wait gives up after
+    // max_polls sleeps (4 * max_polls for a TAA tile) and reports
+    // BMFR_ERROR_SYNC_TIMEOUT instead of running on with incomplete data.
+    // kDefaultMaxPolls unless set by bmfr_debug_sync (include/bmfr_debug.h).
+    int max_polls;
+    // Diagnostics (bmfr_debug_sync): in the one-launch frame, every K1 block
+    // g with g % kDelayStride == kDelayPhase sleeps debug_delay * 127 * 64
+    // shader cycles before it publishes its completion flag, so TAA tiles
+    // really wait.  0: off.
+    int debug_delay;
 };
+constexpr int kDefaultMaxPolls = 1 << 20;
+constexpr int kDelayStride = 61, kDelayPhase = 7;
 
 // BLOCK_OFFSETS (bmfr.cl:267-285), host copy of the device table in
 // bmfr_device.h: the grid shift of frame f is kBlockOffsetTable[f % 16].

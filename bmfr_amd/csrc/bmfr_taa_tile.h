@@ -28,12 +28,48 @@ struct TaaArgs {
     // accumulated colour and reprojected positions once done[g] >= epoch.
     const unsigned* done;
     unsigned epoch;
+    // Page-locked host words (or null): [kSyncPivot] / [kSyncTile] become
+    // nonzero when a K1 pivot wait / a tile's completion-flag wait gave up
+    // (include/bmfr.h BMFR_ERROR_SYNC_TIMEOUT).
+    unsigned* sync_err;
 };
+
+constexpr int kSyncPivot = 0, kSyncTile = 1;
+// One-launch frame: done[g] = epoch (< 2^31) | kDoneTimeout when a pivot wait
+// of block g gave up; the tiles that read the flag report it.
+constexpr unsigned kDoneTimeout = 0x80000000u;
+// An exhausted bounded wait: the kernel runs on (every wave must finish), so
+// the context reports BMFR_ERROR_SYNC_TIMEOUT for this frame instead of
+// handing out its pixels as good.  Cold path: a system-scope vector store to
+// page-locked host memory (idempotent, any number of writers).
+__device__ __forceinline__ void report_sync_timeout(unsigned* err, int which, int frame) {
+    if (err) {
+        __hip_atomic_store(err + which, (unsigned)frame + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+    }
+}
 
 // A COH tile first waits until every K1 block owning a pixel of the tile or
 // its 1-px halo (the blocks of the frame's shifted grid, bmfr.cl:267-285)
-// has published: at most 4 x 2 blocks, one lane each, bounded polls (a
-// protocol error would give wrong pixels, not a wave that never ends).
+// has published: at most 4 x 2 blocks, one lane each.  The polls are bounded
+// (4 * P.max_polls sleeps of 128 cycles): a block that never publishes --
+// a protocol error, or a block parked by the hardware far longer than any
+// frame -- makes the tile report a sync timeout instead of hanging the GPU.
+//
+// Why the hand-off is safe without release / acquire fences (which on gfx942 /
+// gfx950 would write back or invalidate the whole L2 of an XCD): every K1
+// output a tile reads (accumulated colour, reprojected positions) is stored
+// with SC1 (buffer stores with the sc1 policy: written through to memory,
+// the form the AMDGPU memory model uses for agent-scope atomics) and loaded
+// with SC1 (served coherently at device scope, never from another XCD's stale
+// line); each location is written by exactly one block per launch.  The block
+// waits for its own stores to be acknowledged (s_waitcnt vmcnt(0)), meets the
+// work-group barrier (an asm with a memory clobber: no store moves across it)
+// and only then stores its flag.  A tile that reads the flag >= epoch (agent
+// scope, coherent) therefore finds every store of that block performed.  A
+// cache line a tile loads may straddle a neighbouring block that has not
+// finished; the tile never uses those bytes, and any later read of them in
+// the launch is again an SC1 load that does not hit a stale copy.
 __device__ __forceinline__ void wait_k1_blocks(const Params& P, const TaaArgs& T, int x0, int y0, int th) {
     const int2 off = kBlockOffsets[T.frame & 15];
     const int xa = max(x0 - 1, P.ox), xb = min(x0 + 64, P.ox + P.stride - 1);
@@ -45,9 +81,19 @@ __device__ __forceinline__ void wait_k1_blocks(const Params& P, const TaaArgs& T
     if (t < n) {
         const int bx = bxa + t % nx, by = bya + t / nx;
         const unsigned* f = T.done + (by - P.by0) * P.nbx + (bx - P.bx0);
-        for (int k = 0; k < (1 << 22) && __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < T.epoch;
-             ++k)
+        const int limit = 4 * P.max_polls;
+        for (int k = 0;; ++k) {
+            const unsigned v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((v & ~kDoneTimeout) >= T.epoch) {
+                if (v & kDoneTimeout) report_sync_timeout(T.sync_err, kSyncPivot, T.frame);
+                break;
+            }
+            if (k >= limit) {
+                report_sync_timeout(T.sync_err, kSyncTile, T.frame);
+                break;
+            }
             __builtin_amdgcn_s_sleep(2);
+        }
     }
     __syncthreads();
 }

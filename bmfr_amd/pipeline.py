@@ -262,6 +262,16 @@ class Denoiser(_Context):
         check(self.lib.bmfr_halo_status(self.handle, C.byref(v)), "bmfr_halo_status")
         return v.value
 
+    def frame_status(self) -> int:
+        """Waits for the last enqueued frame; the context's sticky report
+        (include/bmfr.h bmfr_frame_status) as a status code, 0 = ok."""
+        return self.lib.bmfr_frame_status(self.handle)
+
+    def debug_sync(self, max_polls: int = -1, k1_delay: int = 0) -> None:
+        """include/bmfr_debug.h bmfr_debug_sync: the kernels' wait bounds and
+        a K1 completion delay, for the frames enqueued from now on."""
+        check(self.lib.bmfr_debug_sync(self.handle, max_polls, k1_delay), "bmfr_debug_sync")
+
     def set_profiling(self, enable: bool, capacity: int = 4096, stride: int = 1) -> None:
         """stride: record only frames whose number is a multiple of it."""
         check(self.lib.bmfr_set_profiling_stride(self.handle, stride), "bmfr_set_profiling_stride")

@@ -45,8 +45,10 @@ typedef enum bmfr_status {
     BMFR_ERROR_OUT_OF_MEMORY = 3,
     BMFR_ERROR_HIP = 4,             /* a HIP runtime call failed (see bmfr_last_hip_error) */
     BMFR_ERROR_NO_DEVICE = 5,
-    BMFR_ERROR_HALO_EXCEEDED = 6    /* tiled context: a frame reprojected past the exchanged halo
+    BMFR_ERROR_HALO_EXCEEDED = 6,   /* tiled context: a frame reprojected past the exchanged halo
                                        (see tile_halo, bmfr_halo_status) */
+    BMFR_ERROR_SYNC_TIMEOUT = 7     /* a fused kernel's bounded wait for another work-group gave up
+                                       (see bmfr_frame_status): that frame's output is not valid */
 } bmfr_status;
 
 /* Feature buffer monomials.  The reference pastes C expressions into the
@@ -276,8 +278,22 @@ bmfr_status bmfr_halo_need(const bmfr_config *cfg, int frame_number, int state_r
 /* Tiled contexts: waits for the last enqueued frame and returns
  * BMFR_ERROR_HALO_EXCEEDED if any frame since frame 0 read reprojection taps
  * past its valid state (see tile_halo), BMFR_OK otherwise; *overshoot
- * (nullable) receives the largest distance in pixels.  Untiled: BMFR_OK. */
+ * (nullable) receives the largest distance in pixels.  Untiled: BMFR_OK.
+ * BMFR_ERROR_SYNC_TIMEOUT takes precedence (see bmfr_frame_status). */
 bmfr_status bmfr_halo_status(bmfr_ctx *ctx, unsigned *overshoot);
+
+/* Waits for the last enqueued frame and returns the context's sticky report:
+ * BMFR_ERROR_SYNC_TIMEOUT if, in any frame since frame 0, a bounded wait of
+ * the fused kernels gave up -- a K1 wave waiting for the pivot column another
+ * wave of its work-group publishes in LDS, or (one-launch frame) a TAA tile
+ * waiting for the completion flags of the K1 blocks under it; the kernels run
+ * to their end regardless (no wave waits forever), so that frame's output and
+ * state are not valid --, else BMFR_ERROR_HALO_EXCEEDED as bmfr_halo_status,
+ * else BMFR_OK.  Every bmfr_process_frame* / bmfr_process_sequence call
+ * returns the same report, without waiting, once the host has seen it, until
+ * frame_number 0 starts a new sequence (frame 0 first waits for every frame
+ * enqueued before it, then clears the reports). */
+bmfr_status bmfr_frame_status(bmfr_ctx *ctx);
 
 /* Device pointer to the last processed frame's output (TAA result, float3,
  * W*H, the buffer the reference reads back at bmfr.cpp:479-480).  Valid until

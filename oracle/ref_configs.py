@@ -136,9 +136,11 @@ FULL_REF_CONFIGS = {
     c.name: c
     for c in (
         RefConfig("f1920x1080_h13", 1920, 1080, frames=17),              # config 2
-        RefConfig("f3840x2160_h13", 3840, 2160, frames=4),               # config 3 (reference default build)
-        RefConfig("f3840x2160_f13", 3840, 2160, half_tmp=0, frames=4),   # config 3, fp32 tmp_data
-        RefConfig("f3840x2160_h16", 3840, 2160, scaled=SCALED_THIRD_ORDER, frames=4),  # config 5 (3rd order)
+        # 4K: 17 frames, so every one of the 16 block-grid offsets (bmfr.cl:267-285) is hit
+        RefConfig("f3840x2160_h13", 3840, 2160, frames=17),              # config 3 (reference default build)
+        RefConfig("f3840x2160_f13", 3840, 2160, half_tmp=0, frames=17),  # config 3, fp32 tmp_data
+        RefConfig("f3840x2160_h16", 3840, 2160, scaled=SCALED_THIRD_ORDER, frames=17),  # config 5 (3rd order)
+        RefConfig("f7680x4320_h13", 7680, 4320, frames=3),               # config 4's frame, untiled
         RefConfig("f1280x720_h13", 1280, 720, frames=60),                # a whole 60-frame sequence
     )
 }

@@ -20,3 +20,29 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda", 0)
+
+
+# Parity numbers the GPU tests measure (worst rel-L2, ulp distances, ...),
+# written as JSON to $BMFR_PARITY_LOG at the end of the session when set --
+# the source of the figures quoted in BASELINE.md / DESIGN.md.
+_PARITY = {}
+
+
+@pytest.fixture(scope="session")
+def parity_log():
+    def record(name: str, values: dict) -> None:
+        _PARITY[name] = values
+    return record
+
+
+def pytest_sessionfinish(session, exitstatus):
+    path = os.environ.get("BMFR_PARITY_LOG")
+    if path and _PARITY:
+        import json
+        old = {}
+        if os.path.exists(path):
+            with open(path) as f:
+                old = json.load(f)
+        old.update(_PARITY)
+        with open(path, "w") as f:
+            json.dump(old, f, indent=1, sort_keys=True)

@@ -1,0 +1,107 @@
+"""The fused kernels' bounded waits report instead of running on silently
+(include/bmfr.h BMFR_ERROR_SYNC_TIMEOUT, bmfr_frame_status; the knobs are
+include/bmfr_debug.h bmfr_debug_sync).
+
+Two waits exist: a K1 wave waiting in LDS for the Householder pivot another
+wave of its work-group publishes (bmfr_fused_cols.hip wait_flag), and, in
+the one-launch frame, a TAA tile waiting for the completion flags of the K1
+blocks under it (bmfr_taa_tile.h wait_k1_blocks)."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+import bmfr_amd
+from bmfr_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(W, H, n):
+    out = []
+    for f in range(n):
+        vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+        _, jit = bmfr_amd.synth_camera(W, H, f)
+        out.append((bmfr_amd.synth_frame_device(W, H, f), vp, jit))
+    return out
+
+
+def _run(den, frames, first=0):
+    for i, (fr, vp, jit) in enumerate(frames):
+        den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, first + i)
+
+
+def _planes(den, W, H):
+    n = W * H
+    return {"result": den.copy_output(torch.empty(3 * n, device="cuda")),
+            "filtered_accumulated": den.copy_state("filtered_accumulated", torch.empty(3 * n, device="cuda")),
+            "noisy_accumulated": den.copy_state("noisy_accumulated", torch.empty(3 * n, device="cuda")),
+            "spp": den.copy_state("spp", torch.empty(n, dtype=torch.uint8, device="cuda")),
+            "prev_frame_pixel": den.copy_state("prev_frame_pixel", torch.empty(2 * n, device="cuda"))}
+
+
+def test_default_bounds_report_ok(gpu):
+    W, H = 3840, 2160
+    den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    _run(den, _frames(W, H, 3))
+    assert den.frame_status() == 0
+
+
+@pytest.mark.parametrize("half_tmp", [1, 0])
+def test_exhausted_waits_report_sync_timeout(half_tmp, gpu):
+    """max_polls = 0: a wait gives up at the first flag that is not ready yet.
+    At 4K thousands of K1 blocks wait for pivots and the TAA tiles in K1's
+    tail wait for blocks still running, so the frame must report; the report
+    is sticky (the next frame's call returns it) until frame 0."""
+    W, H = 3840, 2160
+    den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H,
+                                                use_half_precision_in_tmp_data=half_tmp))
+    frames = _frames(W, H, 3)
+    den.debug_sync(max_polls=0)
+    _run(den, frames[:2])
+    if not half_tmp:  # the f32-tmp_data K1 has no flag waits (work-group barriers only)
+        assert den.frame_status() == 0
+        return
+    assert den.frame_status() == _lib.SYNC_TIMEOUT
+    with pytest.raises(bmfr_amd.BmfrError) as e:
+        _run(den, frames[2:3], first=2)
+    assert e.value.status == _lib.SYNC_TIMEOUT
+    den.debug_sync(max_polls=-1)  # default bounds; frame 0 starts over and clears the report
+    _run(den, frames)
+    assert den.frame_status() == 0
+
+
+def test_sequence_api_reports_sync_timeout(gpu):
+    W, H = 1920, 1080
+    den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    frames = _frames(W, H, 4)
+    den.debug_sync(max_polls=0)
+    den.process_sequence([f for f, _, _ in frames], [(vp, jit) for _, vp, jit in frames], 0)
+    assert den.frame_status() == _lib.SYNC_TIMEOUT
+    den.debug_sync(max_polls=-1)
+    den.process_sequence([f for f, _, _ in frames], [(vp, jit) for _, vp, jit in frames], 0)
+    assert den.frame_status() == 0
+
+
+@pytest.mark.parametrize("W,H", [(3840, 2160), (1920, 1080)])
+def test_delayed_k1_blocks_one_launch_exact(W, H, gpu):
+    """One K1 block in 61 sleeps ~0.3 ms before it raises its completion
+    flag, so the TAA tiles over it really wait on the flags: the one-launch
+    frame must still equal the two-launch frame (profiling on: K1 and K2 as
+    separate launches, no flags) bit for bit on the output and every state
+    plane, and report no timeout."""
+    frames = _frames(W, H, 4)
+    one = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    one.debug_sync(k1_delay=40)
+    two = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    two.set_profiling(True, capacity=16)
+    for i, fr in enumerate(frames):
+        _run(one, [fr], first=i)
+        _run(two, [fr], first=i)
+        a, b = _planes(one, W, H), _planes(two, W, H)
+        for k in a:
+            ia = a[k].view(torch.uint8) if a[k].dtype == torch.uint8 else a[k].view(torch.int32)
+            ib = b[k].view(torch.uint8) if b[k].dtype == torch.uint8 else b[k].view(torch.int32)
+            assert torch.equal(ia, ib), (W, H, i, k, int((ia != ib).sum()))
+    assert one.frame_status() == 0
+    assert len(two.profile()) == len(frames)

@@ -108,13 +108,17 @@ def test_tiled_matches_untiled_bitwise(shape, half, split, kernel_copy, gpu):
                 assert bad.size == 0, (shape, half, f, r, k, len(bad), bad[:3].tolist())
 
 
-def test_8k_tiled_4x2_matches_untiled(gpu):
+@pytest.mark.parametrize("gx,gy", [(4, 2), (2, 4)], ids=["4x2", "2x4"])
+def test_8k_tiled_matches_untiled(gx, gy, gpu):
     """BASELINE config 4 at its own size: 7680x4320 as bench.py's 4x2 grid
-    (halo 64), every frame split into bmfr_process_frame_interior, the
-    bmfr_halo_copy exchange and bmfr_process_frame_border, == the untiled 8K
-    frame bit for bit (output and exchanged state), 3 frames."""
+    and as the 2x4 grid BASELINE.json names (3840x1080 tiles), halo 64,
+    every frame split into bmfr_process_frame_interior, the bmfr_halo_copy
+    exchange and bmfr_process_frame_border, == the untiled 8K frame bit for
+    bit (output and exchanged state), 3 frames.  The untiled 8K frame is
+    itself pinned to the reference kernels (test_gpu_reference_fullsize.py,
+    f7680x4320_h13)."""
     W, H, halo = 7680, 4320, 64
-    grid = TileGrid(W, H, 4, 2, halo=halo)
+    grid = TileGrid(W, H, gx, gy, halo=halo)
     full = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
     tiles = [bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H, tile=grid.tile(r),
                                                    tile_halo=halo)) for r in range(grid.ranks)]

@@ -4,7 +4,7 @@
 production schedule, one launch each, unlike libbmfr's per-kernel
 profiling, which splits K1 and K2), averaged over runs of 10 frames.
 
-  python tools/frame_times.py [W H FRAMES [PASSES]]
+  python tools/frame_times.py [W H FRAMES [PASSES]] [--third-order] [--input-half] [--f32-tmp]
 """
 import os
 import sys
@@ -15,12 +15,15 @@ import torch  # noqa: E402
 
 import bmfr_amd  # noqa: E402
 
-W, H, N = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (3840, 2160, 100)))
-frames = [bmfr_amd.synth_frame_device(W, H, f) for f in range(N)]
-P = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from tool_cfg import parse  # noqa: E402
+
+a, cfg = parse(default_passes=2)
+W, H, N, P = a.W, a.H, a.frames, a.passes
+frames = [a.render(f) for f in range(N)]
 # All passes enqueued back to back (contexts made up front, one synchronize at
 # the end): the GPU never idles between passes.
-dens = [bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H)) for _ in range(P)]
+dens = [bmfr_amd.Denoiser(cfg) for _ in range(P)]
 evs = [[torch.cuda.Event(enable_timing=True) for _ in range(N + 1)] for _ in range(P)]
 torch.cuda.synchronize()
 for rep in range(P):

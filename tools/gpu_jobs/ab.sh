@@ -1,4 +1,4 @@
-# usage: bash tools/gpu_ab.sh "<pytest -k expr or empty>" variant...
+# usage: bash tools/gpu_jobs/ab.sh "<pytest -k expr or empty>" variant...
 set -o pipefail
 mkdir -p gpurun_out
 K="$1"; shift

@@ -1,13 +1,18 @@
-# Round-2 evidence on the GPU box: rocprofv3 kernel stats of the bench command
-# and PMC passes (one counter group per run, each under its own time limit):
-# SQ / TA / I-cache passes and HBM traffic of K1 and K2 as separate launches
-# (tools/k1_frames.py: libbmfr per-kernel events split them), and HBM
-# traffic of the one-launch frame kernel (tools/frame_times.py).
+# Profiling evidence on the GPU box (run through gpurun from the repo root):
+#   bash tools/gpu_jobs/profile.sh OUT [W H [extra k1_frames/frame_times args]]
+# rocprofv3 kernel statistics of the default bench command, then PMC passes
+# (one counter group per run, each under its own time limit): SQ / TA /
+# I-cache passes and HBM traffic of K1 and K2 as separate launches
+# (tools/k1_frames.py: libbmfr per-kernel events split them) and HBM traffic
+# of the one-launch frame kernel (tools/frame_times.py).  Output under
+# gpurun_out/OUT; summarise with tools/prof_summary.py.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/prof_r02e
+O=gpurun_out/${1:-prof}
+W=${2:-3840}; H=${3:-2160}; shift 3 2>/dev/null; X="$*"
 mkdir -p $O
-P="python3 tools/k1_frames.py 3840 2160 12"
+P="python3 tools/k1_frames.py $W $H 12 $X"
+F="python3 tools/frame_times.py $W $H 12 $X"
 step() { local name=$1; shift; timeout -s KILL 150 "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; return $rc; }
 step stats rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-format csv -- python3 bench.py --cpu-frames 0 && \
 step pmcA rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/pmcA -o p --output-format csv -- $P && \
@@ -16,5 +21,5 @@ step pmcC rocprofv3 --pmc SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_
 step pmcD rocprofv3 --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS -d $O/pmcD -o p --output-format csv -- $P && \
 step fetch rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o p --output-format csv -- $P && \
 step write rocprofv3 --pmc WRITE_SIZE -d $O/write -o p --output-format csv -- $P && \
-step fetchF rocprofv3 --pmc FETCH_SIZE -d $O/fetchF -o p --output-format csv -- python3 tools/frame_times.py 3840 2160 12 && \
-step writeF rocprofv3 --pmc WRITE_SIZE -d $O/writeF -o p --output-format csv -- python3 tools/frame_times.py 3840 2160 12
+step fetchF rocprofv3 --pmc FETCH_SIZE -d $O/fetchF -o p --output-format csv -- $F && \
+step writeF rocprofv3 --pmc WRITE_SIZE -d $O/writeF -o p --output-format csv -- $F

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Run a list of GPU steps on the gpurun box, each under its own time limit.
-# Usage: tools/gpu_steps.sh "<secs>:<name>:<command>" ...
+# Usage: tools/gpu_jobs/steps.sh "<secs>:<name>:<command>" ...
 # A step's output goes to gpurun_out/<name>.log.  Any failing step ends the
 # script there (a failure may be a GPU fault: nothing else runs on the GPU
 # after it).

@@ -3,7 +3,7 @@
 profiling events, stride 1), to see how the per-frame cost moves along the
 sequence (spp growth, reprojection acceptance).
 
-  python tools/k1_frames.py [W H FRAMES [PASSES]]
+  python tools/k1_frames.py [W H FRAMES [PASSES]] [--third-order] [--input-half] [--f32-tmp]
 
 With PASSES > 1 the whole sequence runs again from frame 0 in a fresh
 context, back to back (separates a per-frame data effect from the GPU's
@@ -18,11 +18,14 @@ import torch  # noqa: E402
 
 import bmfr_amd  # noqa: E402
 
-W, H, N = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (3840, 2160, 100)))
-PASSES = int(sys.argv[4]) if len(sys.argv) > 4 else 1
-frames = [bmfr_amd.synth_frame_device(W, H, f) for f in range(N)]
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from tool_cfg import parse  # noqa: E402
+
+a, cfg = parse(default_passes=1)
+W, H, N, PASSES = a.W, a.H, a.frames, a.passes
+frames = [a.render(f) for f in range(N)]
 for ps in range(PASSES):
-    den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    den = bmfr_amd.Denoiser(cfg)
     den.set_profiling(True, capacity=N, stride=1)
     for f in range(N):
         vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))

@@ -20,15 +20,19 @@ import torch  # noqa: E402
 
 import bmfr_amd  # noqa: E402
 
-W, H = (int(x) for x in (sys.argv[1:3] if len(sys.argv) > 2 else (3840, 2160)))
-# frames whose K1 phases to report (the stamps hold the last frame's blocks)
-report = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [3]
-cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from tool_cfg import parse  # noqa: E402
+
+# W H [FRAMES] (FRAMES = the last frame whose K1 phases to report; frames
+# 0..FRAMES run twice, the second pass reported) + bench.py's config flags
+a, cfg = parse(default_frames=3)
+W, H = a.W, a.H
+report = [a.frames]
 den = bmfr_amd.Denoiser(cfg)
 G = den.sizes.blocks
 names = ["accumulate_noisy", "min/max scale", "QR", "back-subst", "weighted+blend"]
 # frames rendered up front; a first pass over them untimed (GPU at its working clock)
-frames = [bmfr_amd.synth_frame_device(W, H, f) for f in range(max(report) + 1)]
+frames = [a.render(f) for f in range(max(report) + 1)]
 for f in range(len(frames) * 2):
     fr = frames[f % len(frames)]
     g = f % len(frames)
