@@ -1,7 +1,9 @@
-// image_io.cpp -- OpenEXR (scanline, NONE/RLE/ZIPS/ZIP/PIZ) and PNG I/O over zlib.
-// See image_io.h.  The EXR layout follows the published OpenEXR 2 file
-// format: magic + version, attribute list, per-chunk offset table, chunks of
-// (y, size, data) with each scanline's channels stored in channel-list order.
+// image_io.cpp -- OpenEXR (scanline and tiled, NONE/RLE/ZIPS/ZIP/PIZ/PXR24) and
+// PNG I/O over zlib.  See image_io.h.  The EXR layout follows the published
+// OpenEXR 2 file format: magic + version, attribute list, per-chunk offset
+// table, chunks of (y, size, data) -- tiled files: (tile x, tile y, level x,
+// level y, size, data) -- with each scanline's channels stored in
+// channel-list order.
 #include "image_io.h"
 
 #include <zlib.h>
@@ -39,6 +41,10 @@ struct ExrHeader {
     int x0 = 0, y0 = 0, x1 = -1, y1 = -1;
     int line_order = 0;
     bool tiled = false;
+    // tiled files ("tiles" attribute, tiledesc): tile size, level mode
+    // (0 ONE_LEVEL, 1 MIPMAP_LEVELS, 2 RIPMAP_LEVELS; only level (0, 0) is read)
+    uint32_t tile_w = 0, tile_h = 0;
+    int level_mode = -1;
     int width() const { return x1 - x0 + 1; }
     int height() const { return y1 - y0 + 1; }
 };
@@ -46,9 +52,9 @@ struct ExrHeader {
 int lines_per_chunk(int compression) {
     switch (compression) {
         case BMFR_EXR_NONE: case BMFR_EXR_RLE: case BMFR_EXR_ZIPS: return 1;
-        case BMFR_EXR_ZIP: return 16;
+        case BMFR_EXR_ZIP: case BMFR_EXR_PXR24: return 16;
         case BMFR_EXR_PIZ: return 32;
-        default: return 0;  // PXR24 (5), B44 (6, 7), DWAA/B (8, 9): unsupported
+        default: return 0;  // B44 (6, 7), DWAA/B (8, 9): unsupported
     }
 }
 
@@ -127,11 +133,18 @@ bool parse_header(const std::vector<uint8_t>& file, ExrHeader& h, size_t& end, s
         } else if (name == "lineOrder") {
             if (size < 1) return err = "bad lineOrder attribute", false;
             h.line_order = file[r.p];
+        } else if (name == "tiles" && type == "tiledesc") {
+            if (size < 9) return err = "bad tiles attribute", false;
+            h.tile_w = r.get<uint32_t>();
+            h.tile_h = r.get<uint32_t>();
+            h.level_mode = file[r.p] & 0xf;
         }
         r.p = next;
     }
     end = r.p;
-    if (h.tiled) return err = "tiled OpenEXR files are not supported", false;
+    if (h.tiled && (h.level_mode < 0 || h.level_mode > 2 || h.tile_w == 0 || h.tile_h == 0 ||
+                    h.tile_w > (1u << 16) || h.tile_h > (1u << 16)))
+        return err = "bad or missing tile description", false;
     if (lines_per_chunk(h.compression) == 0) return err = "unsupported OpenEXR compression " + std::to_string(h.compression), false;
     // data window extents in 64-bit (x1 - x0 overflows int for hostile corners)
     const int64_t w64 = (int64_t)h.x1 - h.x0 + 1, h64 = (int64_t)h.y1 - h.y0 + 1;
@@ -518,7 +531,57 @@ bool uncompress(const uint8_t* in, size_t n, int width, int lines, const std::ve
 
 }  // namespace piz
 
-bool decode_chunk(const ExrHeader& h, const uint8_t* data, size_t size, size_t raw_size, int lines,
+// ---------------------------------------------------------------- PXR24 --
+// The published OpenEXR PXR24 scheme, decoder side: per scanline and
+// channel, the samples as integers -- HALF 16 bits, UINT 32 bits, FLOAT the
+// top 24 bits of the float rounded (lossy) -- replaced by their differences
+// from the previous sample of the line, split into byte planes (most
+// significant first, each `width` bytes), all planes zlib-deflated.  The
+// decoded FLOAT is the 24-bit value in the top bits, low byte zero.
+bool pxr24_uncompress(const ExrHeader& h, const uint8_t* in, size_t n, int width, int lines,
+                      std::vector<uint8_t>& raw) {
+    size_t planes = 0;  // bytes per pixel of all channels, packed form
+    for (const Channel& c : h.channels) planes += c.type == kHalf ? 2 : (c.type == kFloat ? 3 : 4);
+    const size_t packed = planes * (size_t)width * lines;
+    std::vector<uint8_t> t(packed);
+    uLongf got = (uLongf)packed;
+    if (uncompress(t.data(), &got, in, (uLong)n) != Z_OK || got != packed) return false;
+    uint8_t* o = raw.data();
+    const uint8_t* p = t.data();
+    for (int y = 0; y < lines; ++y)
+        for (const Channel& c : h.channels) {
+            const size_t w = (size_t)width;
+            uint32_t pixel = 0;
+            if (c.type == kHalf) {
+                for (size_t x = 0; x < w; ++x) {
+                    pixel += (uint32_t)p[x] << 8 | p[w + x];
+                    const uint16_t v = (uint16_t)pixel;
+                    std::memcpy(o + 2 * x, &v, 2);
+                }
+                p += 2 * w;
+                o += 2 * w;
+            } else if (c.type == kFloat) {
+                for (size_t x = 0; x < w; ++x) {
+                    pixel += (uint32_t)p[x] << 24 | (uint32_t)p[w + x] << 16 | (uint32_t)p[2 * w + x] << 8;
+                    std::memcpy(o + 4 * x, &pixel, 4);
+                }
+                p += 3 * w;
+                o += 4 * w;
+            } else {
+                for (size_t x = 0; x < w; ++x) {
+                    pixel += (uint32_t)p[x] << 24 | (uint32_t)p[w + x] << 16 | (uint32_t)p[2 * w + x] << 8 |
+                             p[3 * w + x];
+                    std::memcpy(o + 4 * x, &pixel, 4);
+                }
+                p += 4 * w;
+                o += 4 * w;
+            }
+        }
+    return true;
+}
+
+// One chunk (scanline block, or tile) of `lines` lines x `width` pixels.
+bool decode_chunk(const ExrHeader& h, const uint8_t* data, size_t size, size_t raw_size, int width, int lines,
                   std::vector<uint8_t>& raw) {
     const int compression = h.compression;
     raw.resize(raw_size);
@@ -530,8 +593,9 @@ bool decode_chunk(const ExrHeader& h, const uint8_t* data, size_t size, size_t r
     if (compression == BMFR_EXR_PIZ) {
         std::vector<int> words;
         for (const Channel& c : h.channels) words.push_back(type_bytes(c.type) / 2);
-        return piz::uncompress(data, size, h.width(), lines, words, raw) && raw.size() == raw_size;
+        return piz::uncompress(data, size, width, lines, words, raw) && raw.size() == raw_size;
     }
+    if (compression == BMFR_EXR_PXR24) return pxr24_uncompress(h, data, size, width, lines, raw);
     std::vector<uint8_t> t;
     if (compression == BMFR_EXR_RLE) {
         if (!rle_decode(data, size, t, raw_size)) return false;
@@ -618,37 +682,22 @@ int bmfr_exr_read_rgb(const char* path, int width, int height, float* rgb) {
         if (h.channels.size() != 3) return fail(std::string(path) + ": needs R, G, B channels");
         src[0] = 0, src[1] = 1, src[2] = 2;
     }
-    size_t line_bytes = 0;
-    std::vector<size_t> ch_off(h.channels.size());
-    for (size_t i = 0; i < h.channels.size(); ++i) {
-        ch_off[i] = line_bytes;
-        line_bytes += (size_t)width * type_bytes(h.channels[i].type);
-    }
-    const int lpc = lines_per_chunk(h.compression);
-    const int chunks = (height + lpc - 1) / lpc;
-    if (p > file.size() || (size_t)chunks > (file.size() - p) / 8) return fail(std::string(path) + ": truncated offset table");
-    std::vector<uint8_t> raw;
-    for (int c = 0; c < chunks; ++c) {
-        uint64_t off;
-        std::memcpy(&off, file.data() + p + 8 * (size_t)c, 8);
-        // (compared without overflow: an offset near 2^64 must not wrap)
-        if (file.size() < 8 || off > file.size() - 8) return fail(std::string(path) + ": bad chunk offset");
-        int32_t y, size;
-        std::memcpy(&y, file.data() + off, 4);
-        std::memcpy(&size, file.data() + off + 4, 4);
-        const int line0 = y - h.y0;
-        if (line0 < 0 || line0 >= height || size < 0 || (uint64_t)size > file.size() - off - 8)
-            return fail(std::string(path) + ": bad chunk");
-        const int lines = std::min(lpc, height - line0);
-        if (!decode_chunk(h, file.data() + off + 8, (size_t)size, line_bytes * lines, lines, raw))
-            return fail(std::string(path) + ": corrupt chunk at y=" + std::to_string(y));
+    // Rows [line0, line0 + lines) x columns [x0, x0 + w) of decoded chunk
+    // data (per line: each channel's w samples) into the RGB buffer.
+    auto scatter = [&](const std::vector<uint8_t>& raw, int x0, int w, int line0, int lines) {
+        size_t line_bytes = 0;
+        std::vector<size_t> ch_off(h.channels.size());
+        for (size_t i = 0; i < h.channels.size(); ++i) {
+            ch_off[i] = line_bytes;
+            line_bytes += (size_t)w * type_bytes(h.channels[i].type);
+        }
         for (int l = 0; l < lines; ++l) {
             const uint8_t* line = raw.data() + line_bytes * l;
-            float* dst = rgb + (size_t)(line0 + l) * width * 3;
+            float* dst = rgb + ((size_t)(line0 + l) * width + x0) * 3;
             for (int k = 0; k < 3; ++k) {
                 const Channel& ch = h.channels[src[k]];
                 const uint8_t* s = line + ch_off[src[k]];
-                for (int x = 0; x < width; ++x) {
+                for (int x = 0; x < w; ++x) {
                     float v;
                     if (ch.type == kHalf) {
                         uint16_t u;
@@ -665,6 +714,52 @@ int bmfr_exr_read_rgb(const char* path, int width, int height, float* rgb) {
                 }
             }
         }
+    };
+    size_t px_bytes = 0;  // all channels of one pixel
+    for (const Channel& c : h.channels) px_bytes += type_bytes(c.type);
+    std::vector<uint8_t> raw;
+    if (h.tiled) {
+        // Level (0, 0): the first nx * ny entries of the offset table (tiles
+        // in row-major order; the other levels of a mip / rip map follow).
+        const int64_t nx = ((int64_t)width + h.tile_w - 1) / h.tile_w, ny = ((int64_t)height + h.tile_h - 1) / h.tile_h;
+        if (p > file.size() || (uint64_t)(nx * ny) > (file.size() - p) / 8) return fail(std::string(path) + ": truncated offset table");
+        std::vector<uint8_t> seen((size_t)(nx * ny), 0);
+        for (int64_t c = 0; c < nx * ny; ++c) {
+            uint64_t off;
+            std::memcpy(&off, file.data() + p + 8 * (size_t)c, 8);
+            if (file.size() < 20 || off > file.size() - 20) return fail(std::string(path) + ": bad tile offset");
+            int32_t hd[5];  // tile x, tile y, level x, level y, data size
+            std::memcpy(hd, file.data() + off, 20);
+            if (hd[0] < 0 || hd[0] >= nx || hd[1] < 0 || hd[1] >= ny || hd[2] != 0 || hd[3] != 0 || hd[4] < 0 ||
+                (uint64_t)hd[4] > file.size() - off - 20 || seen[(size_t)(hd[1] * nx + hd[0])])
+                return fail(std::string(path) + ": bad tile");
+            seen[(size_t)(hd[1] * nx + hd[0])] = 1;
+            const int x0 = (int)(hd[0] * (int64_t)h.tile_w), y0 = (int)(hd[1] * (int64_t)h.tile_h);
+            const int w = std::min((int)h.tile_w, width - x0), lines = std::min((int)h.tile_h, height - y0);
+            if (!decode_chunk(h, file.data() + off + 20, (size_t)hd[4], px_bytes * w * lines, w, lines, raw))
+                return fail(std::string(path) + ": corrupt tile " + std::to_string(hd[0]) + "," + std::to_string(hd[1]));
+            scatter(raw, x0, w, y0, lines);
+        }
+        return 0;
+    }
+    const int lpc = lines_per_chunk(h.compression);
+    const int chunks = (height + lpc - 1) / lpc;
+    if (p > file.size() || (size_t)chunks > (file.size() - p) / 8) return fail(std::string(path) + ": truncated offset table");
+    for (int c = 0; c < chunks; ++c) {
+        uint64_t off;
+        std::memcpy(&off, file.data() + p + 8 * (size_t)c, 8);
+        // (compared without overflow: an offset near 2^64 must not wrap)
+        if (file.size() < 8 || off > file.size() - 8) return fail(std::string(path) + ": bad chunk offset");
+        int32_t y, size;
+        std::memcpy(&y, file.data() + off, 4);
+        std::memcpy(&size, file.data() + off + 4, 4);
+        const int line0 = (int)((int64_t)y - h.y0);
+        if ((int64_t)y - h.y0 < 0 || (int64_t)y - h.y0 >= height || size < 0 || (uint64_t)size > file.size() - off - 8)
+            return fail(std::string(path) + ": bad chunk");
+        const int lines = std::min(lpc, height - line0);
+        if (!decode_chunk(h, file.data() + off + 8, (size_t)size, px_bytes * width * lines, width, lines, raw))
+            return fail(std::string(path) + ": corrupt chunk at y=" + std::to_string(y));
+        scatter(raw, 0, width, line0, lines);
     }
     return 0;
 }

@@ -3,11 +3,12 @@
  * Replaces the reference's OpenImageIO calls: read_image_file()
  * (bmfr.cpp:145-163, ImageInput::open + read_image(TypeDesc::FLOAT), 3
  * channels) and the PNG output of bmfr.cpp:519-553 (ImageOutput, FLOAT ->
- * 8 bit).  Self-contained over zlib: scanline OpenEXR 2.x single-part files
- * with HALF / FLOAT / UINT channels and NONE, RLE, ZIPS, ZIP or PIZ
- * compression (the formats of the BMFR dataset and of common renderers;
- * PXR24, B44 and DWA and tiled / deep / multi-part files are rejected with
- * an error); writer: FLOAT RGB, NONE or ZIP.
+ * 8 bit).  Self-contained over zlib: OpenEXR 2.x single-part files, scanline
+ * or tiled (one-level; the full-resolution level of mip / rip maps), with
+ * HALF / FLOAT / UINT channels and NONE, RLE, ZIPS, ZIP, PIZ or PXR24
+ * compression (the formats of the BMFR dataset and of common renderers; B44
+ * and DWA and deep / multi-part files are rejected with an error); writer:
+ * FLOAT RGB, NONE or ZIP.
  */
 #ifndef BMFR_IMAGE_IO_H
 #define BMFR_IMAGE_IO_H
@@ -23,7 +24,8 @@ typedef enum bmfr_exr_compression {
     BMFR_EXR_RLE = 1,
     BMFR_EXR_ZIPS = 2,
     BMFR_EXR_ZIP = 3,
-    BMFR_EXR_PIZ = 4  /* read only */
+    BMFR_EXR_PIZ = 4,   /* read only */
+    BMFR_EXR_PXR24 = 5  /* read only (lossy: FLOAT samples keep 24 bits) */
 } bmfr_exr_compression;
 
 /* Size of an EXR file's data window.  0 on success, else -1 (message via

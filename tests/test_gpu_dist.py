@@ -1,5 +1,6 @@
-"""The multi-rank tiled path as bench.py runs it, in two processes on one GPU
-(gloo with host-staged messages stands in for RCCL): each rank denoises its
+"""The multi-rank tiled path as bench.py runs it, in 2, 4 and 8 processes on
+one GPU (gloo with host-staged messages stands in for RCCL; 8 ranks = the
+4x2 grid of the driver's 8-GPU node): each rank denoises its
 tile with bmfr_process_frame_interior, the halo exchange on its own stream
 (DistTransport.exchange_ctx: bmfr_halo_copy pack, isend/irecv, unpack) and
 bmfr_process_frame_border, and must reproduce its tile of the untiled frame
@@ -69,7 +70,7 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])  # 8: the driver node's 4x2 plan (bench.py --gpus 8), rehearsed
 def test_two_process_tiled_frames_match_untiled(world, gpu):
     import torch.multiprocessing as mp
     with socket.socket() as s:
@@ -80,7 +81,7 @@ def test_two_process_tiled_frames_match_untiled(world, gpu):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    results = dict(q.get(timeout=240) for _ in procs)
+    results = dict(q.get(timeout=400) for _ in procs)
     for p in procs:
         p.join(timeout=60)
     assert all(v == [] for v in results.values()), results

@@ -105,3 +105,49 @@ def test_delayed_k1_blocks_one_launch_exact(W, H, gpu):
             assert torch.equal(ia, ib), (W, H, i, k, int((ia != ib).sum()))
     assert one.frame_status() == 0
     assert len(two.profile()) == len(frames)
+
+
+def test_delayed_k1_blocks_tiled_border_launch_exact(gpu):
+    """Tiled contexts run a frame's border ring of K1 blocks and the tile's TAA
+    in one launch (completion flags; the launch's last work-group forwards
+    the reach report after every ring block): with one K1 block in 61
+    delayed, every tile of a 4x2 grid still equals the untiled frame bit for
+    bit, through the interior / exchange / border split, and reports
+    neither a timeout nor a halo overshoot."""
+    from bmfr_amd.tiling import LoopbackTransport, TileGrid
+    W, H, halo = 960, 544, 40
+    grid = TileGrid(W, H, 4, 2, halo=halo)
+    full = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    tiles = [bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H, tile=grid.tile(r), tile_halo=halo))
+             for r in range(grid.ranks)]
+    for d in tiles:
+        d.debug_sync(k1_delay=40)
+    loop = LoopbackTransport(grid)
+    prev = [None] * grid.ranks
+    for f in range(6):
+        vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+        _, jit = bmfr_amd.synth_camera(W, H, f)
+        fr = bmfr_amd.synth_frame_device(W, H, f)
+        full.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, f)
+        inps = [bmfr_amd.synth_region_device(W, H, d.region, f) for d in tiles]
+        kws = [dict(prev_normals=p["normals"], prev_positions=p["positions"]) if p else {} for p in prev]
+        args = [(i["noisy"], i["normals"], i["positions"], i["albedo"], vp, jit, f) for i in inps]
+        if f == 0:
+            for r in range(grid.ranks):
+                tiles[r].process_frame(*args[r], **kws[r])
+        else:
+            for r in range(grid.ranks):
+                tiles[r].process_frame_interior(*args[r], **kws[r])
+            loop.exchange_all_ctx(tiles, f)
+            for r in range(grid.ranks):
+                tiles[r].process_frame_border(*args[r], **kws[r])
+        prev = inps
+        want = full.copy_output(torch.empty(3 * W * H, device="cuda")).view(H, W, 3)
+        for r, d in enumerate(tiles):
+            assert d.frame_status() == 0
+            rx, ry, rw, rh = d.region
+            x, y, w, h = grid.tile(r)
+            got = d.copy_output(torch.empty(3 * rw * rh, device="cuda")).view(rh, rw, 3)
+            a = got[y - ry:y - ry + h, x - rx:x - rx + w].contiguous().view(torch.int32)
+            b = want[y:y + h, x:x + w].contiguous().view(torch.int32)
+            assert torch.equal(a, b), (f, r, int((a != b).sum()))

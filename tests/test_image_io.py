@@ -1,9 +1,11 @@
 """EXR / PNG I/O of the host (host/image_io.cpp), checked
 against an independent numpy + zlib implementation of the same published
-formats written here: OpenEXR 2 scanline files (HALF / FLOAT channels,
-NONE / RLE / ZIPS / ZIP compression, and PIZ through the independent encoder
-tests/exr_piz_py.py) and 8-bit RGB PNG.  EXR parity is unpinned: no OpenEXR
-library and no reference .exr file exist here."""
+formats written here: OpenEXR 2 scanline and tiled files (HALF / FLOAT
+channels, NONE / RLE / ZIPS / ZIP / PXR24 compression, and PIZ through the
+independent encoder tests/exr_piz_py.py; one-level and mip-mapped tiles) and
+8-bit RGB PNG.  EXR parity is unpinned: no OpenEXR library and no reference
+.exr file exist here, so the reader is only as right as these encoders'
+reading of the published format."""
 from __future__ import annotations
 
 import ctypes as C
@@ -65,36 +67,105 @@ def _rle(data: bytes) -> bytes:
     return bytes(out)
 
 
-def write_exr_py(path, img: dict, compression: int, half: bool):
+def f24(a: np.ndarray) -> np.ndarray:
+    """PXR24's float -> 24-bit conversion (published OpenEXR scheme): the top
+    24 bits of the float, rounded half up in the mantissa, not rounding into
+    infinity; NaN stays NaN."""
+    i = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.int64)
+    s, e, m = i & 0x80000000, i & 0x7f800000, i & 0x007fffff
+    r = ((e | m) + (m & 0x80)) >> 8
+    r = np.where(r >= 0x7f8000, (e | m) >> 8, r)
+    m8 = m >> 8
+    special = np.where(m != 0, (e >> 8) | m8 | (m8 == 0), e >> 8)
+    return (np.where(e == 0x7f800000, special, r) | (s >> 8)).astype(np.int64)
+
+
+def f24_values(a: np.ndarray) -> np.ndarray:
+    """What a PXR24 FLOAT sample decodes to: the 24 bits, low byte zero."""
+    return (f24(a) << 8).astype(np.uint32).view(np.float32).reshape(np.shape(a))
+
+
+def _pxr24(img, names, y0, lines, x0, w, half):
+    """One PXR24 chunk: per line and channel, sample differences split into
+    byte planes (most significant first), deflated."""
+    out = bytearray()
+    for y in range(y0, y0 + lines):
+        for n in names:
+            row = np.ascontiguousarray(img[n][y, x0:x0 + w])
+            if half:
+                v = row.astype(np.float16).view(np.uint16).astype(np.int64)
+                nb = 2
+            else:
+                v = f24(row)
+                nb = 3
+            d = np.diff(np.concatenate([[0], v])) & 0xffffffff
+            for k in range(nb):
+                out += ((d >> (8 * (nb - 1 - k))) & 255).astype(np.uint8).tobytes()
+    return zlib.compress(bytes(out))
+
+
+RAW_CHUNKS = []  # (level, y0, lines, x0, w) of the chunks write_exr_py stored uncompressed
+
+
+def _chunk_data(img, names, dt, compression, y0, lines, x0, w, half, level=0):
+    raw = b"".join(np.ascontiguousarray(img[n][y, x0:x0 + w]).astype(dt).tobytes()
+                   for y in range(y0, y0 + lines) for n in names)
+    if compression == 1:
+        data = _rle(_predict(raw))
+    elif compression in (2, 3):
+        data = zlib.compress(_predict(raw))
+    elif compression == 4:
+        data = piz_compress(raw, w, lines, [1 if half else 2] * len(names))
+    elif compression == 5:
+        data = _pxr24(img, names, y0, lines, x0, w, half)
+    else:
+        data = raw
+    if compression and len(data) >= len(raw):  # OpenEXR stores such a chunk as it is
+        RAW_CHUNKS.append((level, y0, lines, x0, w))
+        return raw
+    return data
+
+
+def write_exr_py(path, img: dict, compression: int, half: bool, tile=None, mipmap=False):
     """img: channel name -> (H, W) float array.  Channels are stored sorted by
-    name.  compression 0 NONE, 1 RLE, 2 ZIPS, 3 ZIP, 4 PIZ."""
+    name.  compression 0 NONE, 1 RLE, 2 ZIPS, 3 ZIP, 4 PIZ, 5 PXR24.
+    tile = (tw, th): a tiled file (ONE_LEVEL, or MIPMAP_LEVELS round-down
+    with mipmap=True: the lower levels follow level 0, box-filtered)."""
     names = sorted(img)
     H, W = img[names[0]].shape
     ptype, dt = (1, np.float16) if half else (2, np.float32)
     chl = b"".join(n.encode() + b"\0" + struct.pack("<iIii", ptype, 0, 1, 1) for n in names) + b"\0"
     box = struct.pack("<iiii", 0, 0, W - 1, H - 1)
-    hdr = (struct.pack("<II", 20000630, 2) + _attr("channels", "chlist", chl) +
+    version = 2 | (0x200 if tile else 0)
+    hdr = (struct.pack("<II", 20000630, version) + _attr("channels", "chlist", chl) +
            _attr("compression", "compression", bytes([compression])) + _attr("dataWindow", "box2i", box) +
            _attr("displayWindow", "box2i", box) + _attr("lineOrder", "lineOrder", b"\0") +
            _attr("pixelAspectRatio", "float", struct.pack("<f", 1)) +
            _attr("screenWindowCenter", "v2f", struct.pack("<ff", 0, 0)) +
-           _attr("screenWindowWidth", "float", struct.pack("<f", 1)) + b"\0")
-    lpc = {0: 1, 1: 1, 2: 1, 3: 16, 4: 32}[compression]
+           _attr("screenWindowWidth", "float", struct.pack("<f", 1)))
+    if tile:
+        hdr += _attr("tiles", "tiledesc", struct.pack("<IIB", tile[0], tile[1], 1 if mipmap else 0))
+    hdr += b"\0"
     chunks = []
-    for y0 in range(0, H, lpc):
-        raw = b"".join(np.ascontiguousarray(img[n][y, :]).astype(dt).tobytes()
-                       for y in range(y0, min(H, y0 + lpc)) for n in names)
-        if compression == 1:
-            data = _rle(_predict(raw))
-        elif compression in (2, 3):
-            data = zlib.compress(_predict(raw))
-        elif compression == 4:
-            data = piz_compress(raw, W, min(H, y0 + lpc) - y0, [1 if half else 2] * len(names))
-        else:
-            data = raw
-        if len(data) >= len(raw):
-            data = raw
-        chunks.append(struct.pack("<ii", y0, len(data)) + data)
+    if tile:
+        tw, th = tile
+        levels = [img]
+        while mipmap and max(levels[-1][names[0]].shape) > 1:
+            h2, w2 = (max(1, d // 2) for d in levels[-1][names[0]].shape)
+            levels.append({n: levels[-1][n][:2 * h2:2, :2 * w2:2][:h2, :w2] for n in names})
+        for lv, im in enumerate(levels):
+            lh, lw = im[names[0]].shape
+            for ty in range((lh + th - 1) // th):
+                for tx in range((lw + tw - 1) // tw):
+                    x0, y0 = tx * tw, ty * th
+                    w, lines = min(tw, lw - x0), min(th, lh - y0)
+                    data = _chunk_data(im, names, dt, compression, y0, lines, x0, w, half, lv)
+                    chunks.append(struct.pack("<iiiii", tx, ty, lv, lv, len(data)) + data)
+    else:
+        lpc = {0: 1, 1: 1, 2: 1, 3: 16, 4: 32, 5: 16}[compression]
+        for y0 in range(0, H, lpc):
+            data = _chunk_data(img, names, dt, compression, y0, min(H, y0 + lpc) - y0, 0, W, half)
+            chunks.append(struct.pack("<ii", y0, len(data)) + data)
     off = len(hdr) + 8 * len(chunks)
     table = b""
     for c in chunks:
@@ -247,3 +318,75 @@ def test_exr_piz_shapes(tmp_path, shape, half):
     assert lib().bmfr_exr_read_rgb(path.encode(), W, H, out.ctypes.data) == 0, lib().bmfr_io_error()
     want = img.astype(np.float16).astype(np.float32) if half else img
     np.testing.assert_array_equal(out, want)
+
+
+@pytest.mark.parametrize("half", [False, True])
+@pytest.mark.parametrize("shape", [(41, 29), (16, 16), (1, 70), (33, 1)])
+def test_exr_pxr24(tmp_path, shape, half):
+    """PXR24 (OpenImageIO reads it, bmfr.cpp:145-163): lossless for HALF,
+    FLOAT samples rounded to 24 bits (f24_values); partial 16-line chunks."""
+    H, W = shape
+    img = np.random.default_rng(H + W).normal(0, 3, (H, W, 3)).astype(np.float32)
+    img[0, 0] = [np.inf, -0.0, np.float32(1.0 + 2 ** -16)]  # the dropped byte's top bit: rounds up
+    img[-1, -1] = [np.nan, 65504.0, np.float32(3.4028235e38)]  # NaN; no rounding into infinity
+    chans = {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2]}
+    path = str(tmp_path / "pxr24.exr")
+    RAW_CHUNKS.clear()
+    write_exr_py(path, chans, 5, half)
+    out = np.empty_like(img)
+    assert lib().bmfr_exr_read_rgb(path.encode(), W, H, out.ctypes.data) == 0, lib().bmfr_io_error()
+    want = img.astype(np.float16).astype(np.float32) if half else f24_values(img)
+    for _, y0, n, x0, w in RAW_CHUNKS if not half else []:  # FLOAT chunks stored uncompressed: exact
+        want[y0:y0 + n, x0:x0 + w] = img[y0:y0 + n, x0:x0 + w]
+    np.testing.assert_array_equal(out, want)
+
+
+@pytest.mark.parametrize("comp", [0, 1, 3, 4, 5])
+@pytest.mark.parametrize("tile,mipmap", [((16, 16), False), ((32, 8), False), ((64, 64), False),
+                                         ((16, 16), True)])
+def test_exr_tiled(tmp_path, comp, tile, mipmap):
+    """Tiled single-part files (renderer output): partial edge tiles, a tile
+    larger than the image, and a mip map whose full-resolution level is read."""
+    img = _img(37, 53, seed=comp)
+    chans = {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2], "A": np.ones(img.shape[:2], np.float32)}
+    path = str(tmp_path / "tiled.exr")
+    RAW_CHUNKS.clear()
+    write_exr_py(path, chans, comp, False, tile=tile, mipmap=mipmap)
+    H, W, _ = img.shape
+    w, h, c = C.c_int(), C.c_int(), C.c_int()
+    assert lib().bmfr_exr_info(path.encode(), C.byref(w), C.byref(h), C.byref(c)) == 0
+    assert (w.value, h.value, c.value) == (W, H, 4)
+    out = np.empty_like(img)
+    assert lib().bmfr_exr_read_rgb(path.encode(), W, H, out.ctypes.data) == 0, lib().bmfr_io_error()
+    want = f24_values(img) if comp == 5 else img.copy()
+    for lv, y0, n, x0, w in RAW_CHUNKS:  # level-0 tiles stored uncompressed are exact
+        if lv == 0:
+            want[y0:y0 + n, x0:x0 + w] = img[y0:y0 + n, x0:x0 + w]
+    np.testing.assert_array_equal(out, want)
+
+
+def test_exr_tiled_rejects_bad_tiles(tmp_path):
+    """A tiled file without a tile description, or a tile of another level
+    where level (0, 0) is expected, is rejected with a message."""
+    img = _img(8, 8)
+    chans = {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2]}
+    path = tmp_path / "t.exr"
+    write_exr_py(str(path), chans, 0, False, tile=(4, 4))
+    data = path.read_bytes()
+    i = data.index(b"tiles\0tiledesc\0")
+    no_desc = data[:i] + b"tileX\0" + data[i + 6:]  # attribute renamed: no tile description
+    out = np.empty_like(img)
+    (tmp_path / "nodesc.exr").write_bytes(no_desc)
+    assert lib().bmfr_exr_read_rgb(str(tmp_path / "nodesc.exr").encode(), 8, 8, out.ctypes.data) != 0
+    assert b"tile" in lib().bmfr_io_error()
+    # the first tile's level x -> 1
+    p = 8
+    while data[p]:  # attributes: name, type, size, value
+        e2 = data.index(b"\0", data.index(b"\0", p) + 1)
+        p = e2 + 5 + struct.unpack_from("<i", data, e2 + 1)[0]
+    first = struct.unpack_from("<Q", data, p + 1)[0]  # the offset table follows the terminating null
+    b = bytearray(data)
+    struct.pack_into("<i", b, first + 8, 1)
+    (tmp_path / "level.exr").write_bytes(bytes(b))
+    assert lib().bmfr_exr_read_rgb(str(tmp_path / "level.exr").encode(), 8, 8, out.ctypes.data) != 0
+    assert b"bad tile" in lib().bmfr_io_error()

@@ -4,9 +4,9 @@ CPU side):
 
 * the CPU restatement oracle/bmfr_oracle.c, all five stages over several
   configurations (tests/native/oracle_asan_main.c);
-* the EXR reader host/image_io.cpp (PIZ decoder included) -- the one
-  component that parses external files -- over a corpus of malformed files
-  derived from valid ones:
+* the EXR reader host/image_io.cpp (PIZ and PXR24 decoders, scanline and
+  tiled files) -- the one component that parses external files -- over a
+  corpus of malformed files derived from valid ones:
   every truncation length of a small file, seeded random byte corruption,
   and hand-made hostile headers (huge chunk offsets, attribute sizes past
   the end, empty single-byte attributes, overflowing data windows).
@@ -88,20 +88,23 @@ def test_exr_reader_malformed_corpus_under_asan_ubsan(tmp_path):
     img = _img(H=7, W=11)
     corpus = []
     rng = np.random.default_rng(0x424D4652)
-    for comp, half in ((0, False), (1, False), (2, True), (3, False), (4, False), (4, True)):
-        src = tmp_path / f"valid_{comp}_{int(half)}.exr"
-        write_exr_py(str(src), {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2]}, comp, half=half)
+    for comp, half, tile in ((0, False, None), (1, False, None), (2, True, None), (3, False, None),
+                             (4, False, None), (4, True, None), (5, False, None), (5, True, None),
+                             (3, False, (4, 4)), (4, False, (8, 2)), (5, False, (4, 4))):
+        name = f"{comp}_{int(half)}" + (f"_t{tile[0]}x{tile[1]}" if tile else "")
+        src = tmp_path / f"valid_{name}.exr"
+        write_exr_py(str(src), {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2]}, comp, half=half, tile=tile)
         data = src.read_bytes()
         corpus.append(str(src))
         for n in range(0, len(data), max(1, len(data) // 97)):  # truncations
-            p = tmp_path / f"trunc_{comp}_{int(half)}_{n}.exr"
+            p = tmp_path / f"trunc_{name}_{n}.exr"
             p.write_bytes(data[:n])
             corpus.append(str(p))
         for k in range(120):  # 1..8 corrupted bytes anywhere
             b = bytearray(data)
             for i in rng.integers(0, len(b), rng.integers(1, 9)):
                 b[i] = int(rng.integers(0, 256))
-            p = tmp_path / f"flip_{comp}_{int(half)}_{k}.exr"
+            p = tmp_path / f"flip_{name}_{k}.exr"
             p.write_bytes(bytes(b))
             corpus.append(str(p))
     hostile = _hostile(tmp_path)

@@ -81,7 +81,10 @@ def pmc(d, counter):
     return {k: statistics.mean(v) for k, v in per.items()}
 
 
-KERNELS = {"K1 k_fused_cols": "k_fused_cols<4, 6, float>", "K2 k_fused_taa": "k_fused_taa<float>"}
+# K1 / K2 of the default configuration; K1_NAME / K2_NAME select another one
+# (e.g. "k_fused_cols<4, 9, _Float16>" / "k_fused_taa<_Float16>" for config 5).
+KERNELS = {"K1 k_fused_cols": os.environ.get("K1_NAME", "k_fused_cols<4, 6, float>"),
+           "K2 k_fused_taa": os.environ.get("K2_NAME", "k_fused_taa<float>")}
 
 
 def sq(dirs):
