@@ -13,7 +13,10 @@ active on every timed frame).
 
 The N = 1 line also carries the metric's other sizes, untiled on the same
 GPU: `ms_per_frame_1080p` (1920x1080) and `ms_per_frame_8k` (7680x4320, the
-1-GPU point of the north star's scaling target), and
+1-GPU point of the north star's scaling target); BASELINE's other 4K
+configurations with their own rooflines: `ms_per_frame_cfg5` (config 5:
+half input planes, 3rd-order features, B = 16) and `ms_per_frame_f32tmp`
+(f32 tmp_data); and
 `ms_per_frame_sequence`: the same 4K frames through bmfr_process_sequence
 (K2 of frame f inside K1 of f + 1's launch, as the reference's frame loop
 enqueues every frame without waiting).  `value` stays the per-frame API's
@@ -109,6 +112,8 @@ def parse():
     ap.add_argument("--no-sequence", action="store_true", help="skip the sequence-mode field of the N = 1 line")
     ap.add_argument("--no-8k", action="store_true", help="skip the untiled 7680x4320 line (N = 1) / the 1-GPU "
                                                          "reference time (N > 1)")
+    ap.add_argument("--no-variants", action="store_true",
+                    help="skip the N = 1 line's config-5 (half inputs, B = 16) and f32-tmp_data fields")
     ap.add_argument("--frames-8k", type=int, default=30, help="timed frames of the untiled 8K line (N = 1)")
     ap.add_argument("--cpu-frames", type=int, default=12,
                     help="timed CPU-oracle frames (0 = skip); 12 at 4K is ~10 s of host work")
@@ -379,6 +384,18 @@ def side_line(r):
             "psnr_db": round(r["psnr"], 2)}
 
 
+def variant_line(r, s: int, W: int, H: int, workload: str, kernel: str):
+    """A same-size configuration field of the N = 1 line (BASELINE config 5,
+    f32 tmp_data): side_line plus the roofline of its one-launch frame kernel
+    (the frame's 18 s + 74 B/px over the kernel's HIP-event duration)."""
+    fb = frame_bytes_per_px(s) * W * H
+    fa = fb / (r["frame_kernel_ms"] * 1e-3) / 1e9
+    return dict(side_line(r), workload=workload,
+                roofline={"bound": "hbm", "achieved": round(fa, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(fa / HBM_PEAK_GBS, 4), "kernel": kernel + " (K1 + K2 of the frame, one launch)",
+                          "algorithmic_bytes_per_launch": fb, "launch_ms": round(r["frame_kernel_ms"], 4)})
+
+
 def spin_up(a, cfg, local, frames, cams):
     """Untimed: the same frames through a scratch context for --spin-up
     seconds before the measured context starts; returns that context, whose
@@ -461,6 +478,20 @@ def main():
         r8k = run_sequence(a, 7680, 4320, (0, 0, 7680, 4320), None, 0, 1, dev, backend, n8, a.warmup,
                            per_frame=not a.sequence)
         r8k["steps"] = n8
+    # The other same-size configurations BASELINE.json names (N = 1): config 5
+    # (fp16 feature buffers + 3rd-order features) and config 3 with f32
+    # tmp_data, per-frame API, each with its own roofline.
+    rvar = {}
+    if world == 1 and not a.no_variants and not a.sequence:
+        import copy
+        for key, upd in (("cfg5", dict(third_order=True, input_half=True, half_tmp=1)),
+                         ("f32tmp", dict(third_order=False, input_half=False, half_tmp=0))):
+            if all(getattr(a, k) == v for k, v in upd.items()):
+                continue  # the main line already is this configuration
+            b = copy.copy(a)
+            b.__dict__.update(upd)
+            rvar[key] = (b, run_sequence(b, W, H, (0, 0, W, H), None, 0, 1, dev, backend, a.steps, a.warmup,
+                                         per_frame=True))
     ranks = None
     if world > 1 and r["split"] is not None:
         keys = ("interior_ms", "exchange_ms", "border_ms", "frame_ms", "halo_bytes_sent", "halo_overshoot_px")
@@ -488,13 +519,14 @@ def main():
         # (K1 blocks + TAA tiles), the dominant -- only -- kernel of the timed
         # region; its roofline is the frame's algorithmic bytes over its
         # duration, and K1's own (timed apart, untimed pass) is roofline_k1.
-        one_launch = r["frame_kernel_ms"] is not None and a.half_tmp
+        one_launch = r["frame_kernel_ms"] is not None
         if one_launch:
             fb = frame_bytes_per_px(s) * tile_px
             fa = fb / (r["frame_kernel_ms"] * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(fa, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(fa / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(workload + "_frame"),
-                    "kernel": "k_fused_cols_taa<..., SAME = true> (K1 + K2 of the frame, one launch)",
+                    "kernel": ("k_fused_cols_taa<..., SAME = true>" if a.half_tmp else "k_fused_rows_taa<...>")
+                              + " (K1 + K2 of the frame, one launch)",
                     "algorithmic_bytes_per_launch": fb, "launch_ms": round(r["frame_kernel_ms"], 4),
                     "limiter": "K1 blocks: latency of phase-1 gathers and of the fit's pivot chain, VALU issue "
                                "(roofline_k1); TAA tiles: texture path / latency (roofline_k2) -- not HBM"}
@@ -545,8 +577,20 @@ def main():
         if r1 is not None:
             line["ms_per_frame_1gpu"] = side_line(r1)
             line["speedup_vs_1gpu"] = round(r1["ms_per_frame"] / ms_per_frame, 3)
+        if world > 1:
+            # `value` here is the whole W x H frame cut into tiles; the N = 1
+            # line's `value` is the 4K frame -- the 1-GPU point of this curve is
+            # ms_per_frame_1gpu (and the N = 1 line's ms_per_frame_8k)
+            line["scaling_reference"] = (f"ms_per_frame_1gpu ({W}x{H} untiled, rank 0's GPU)"
+                                         if a.scaling == "strong" else "none (weak scaling: one tile per GPU)")
         if ranks is not None:
             line["ranks"] = ranks
+        for key, (b, rv) in rvar.items():
+            vs = 2 if b.input_half else 4
+            wl = f"bmfr_{W}x{H}_B{rv['cfg'].buffer_count}_{'half' if b.half_tmp else 'f32'}tmp" + \
+                 ("_f16in" if b.input_half else "")
+            line[f"ms_per_frame_{key}"] = variant_line(rv, vs, W, H, wl, "k_fused_cols_taa<..., SAME = true>"
+                                                       if b.half_tmp else "k_fused_rows_taa<...>")
         if world == 1 and a.cpu_frames > 0:
             line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_frames, a.seed)
         print(json.dumps(line), flush=True)

@@ -643,6 +643,19 @@ hipError_t noise_for_frame(bmfr_ctx* c, const Params& P, hipStream_t s, int f, f
     return hipSuccess;
 }
 
+// One-launch frames: the next epoch of the completion flags (never 0 and
+// below 2^31, the flag's top bit carries a timeout; flags reset on wrap).
+bmfr_status next_epoch(bmfr_ctx* c, hipStream_t s, bmfr::FusedArgs* A) {
+    if (++c->epoch == bmfr::kDoneTimeout) {
+        const bmfr_status st = hip_status(hipMemsetAsync(c->done, 0, done_bytes(c), s));
+        if (st != BMFR_OK) return st;
+        c->epoch = 1;
+    }
+    A->done = c->done;
+    A->epoch = c->epoch;
+    return BMFR_OK;
+}
+
 // PART 0: noise table + interior blocks.  PART 1: border blocks + K2 (+ swap).
 // PART 2: everything (bmfr_process_frame).
 bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in, const float* m,
@@ -674,15 +687,7 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
     if (part == 2) {
         if (bmfr::fused_supported(P) && (st = hip_status(noise_for_frame(c, P, s, frame_number, &A.noise_table))))
             return st;
-        if (c->done && !ev) {  // one launch: the next epoch (never 0; flags reset on wrap)
-            if (++c->epoch == bmfr::kDoneTimeout) {  // the flag's top bit carries a timeout
-                if ((st = hip_status(hipMemsetAsync(c->done, 0, done_bytes(c), s))))
-                    return st;
-                c->epoch = 1;
-            }
-            A.done = c->done;
-            A.epoch = c->epoch;
-        }
+        if (c->done && !ev && (st = next_epoch(c, s, &A)) != BMFR_OK) return st;  // one launch
         st = hip_status(bmfr::launch_fused_frame(P, s, A, ev ? ev[1] : nullptr));
         if (st != BMFR_OK) return st;
     } else {
@@ -709,9 +714,15 @@ bmfr_status process_part(bmfr_ctx* c, void* stream, const bmfr_frame_inputs* in,
             if (R.ring == 0) R.ring = -1;  // nothing outside the interior
             R.rx0 = ix0, R.rx1 = ix1, R.ry0 = iy0, R.ry1 = iy1;
         }
-        if ((st = hip_status(bmfr::launch_fused_k1_blocks(R, s, A))) != BMFR_OK) return st;
-        if (ev) (void)hipEventRecord(ev[1], s);
-        if ((st = hip_status(bmfr::launch_fused_k2(P, s, A))) != BMFR_OK) return st;
+        if (c->done && !ev && bmfr::frame_fused_supported(R)) {
+            // the ring's K1 blocks and the tile's TAA in one launch (completion flags)
+            if ((st = next_epoch(c, s, &A)) != BMFR_OK) return st;
+            if ((st = hip_status(bmfr::launch_fused_frame_one(R, s, A))) != BMFR_OK) return st;
+        } else {
+            if ((st = hip_status(bmfr::launch_fused_k1_blocks(R, s, A))) != BMFR_OK) return st;
+            if (ev) (void)hipEventRecord(ev[1], s);
+            if ((st = hip_status(bmfr::launch_fused_k2(P, s, A))) != BMFR_OK) return st;
+        }
         c->pending_frame = -1;
         c->pending_prof_slot = -1;
     }

@@ -39,7 +39,11 @@ typedef __amdgpu_buffer_rsrc_t CohPlane;
 __device__ __forceinline__ CohPlane coh_plane(const void* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, -1, 0x00020000);
 }
+#ifdef BMFR_PROBE_NOSC1
+constexpr int kSc1 = 0;  // timing probe only (tools/ab.py variants): plain hand-off, results not guaranteed
+#else
 constexpr int kSc1 = 16;  // buffer instruction cache-policy bit SC1
+#endif
 __device__ __forceinline__ f3 ld3_coh(CohPlane r, uint32_t i) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, i * 12u, 0, kSc1);
     return f3{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2])};

@@ -20,6 +20,7 @@
 #include <utility>
 
 #include "bmfr_launch.h"
+#include "bmfr_taa_tile.h"
 #include "bmfr_wave.h"
 
 namespace bmfr {
@@ -52,6 +53,8 @@ struct K1Lds {
     float R[(B - 2) * (B - 2) * 3];      // R[x][y][ch], x = column
     float weights[(B - 3) * 3];
     float mm[3 * (B - 3)];               // per scaled feature: min, max, 1/(max-min)
+    int flag;                            // one-launch frame: index of this block's completion flag
+    int delay;                           // Params::debug_delay (diagnostics)
 };
 
 // ---------------------------------------------------------------------------
@@ -284,12 +287,15 @@ __device__ __forceinline__ void back_substitute(K1Lds<B>& L, int t) {
     if (x < B - 3) L.weights[x * 3 + ch] = R[((RE - 1) * RE + x) * 3 + ch];
 }
 
-template <int NS, int FS, class IN>
-__global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
+// One K1 work-group (block g of the launch) on the LDS area L.  COH: the TAA
+// tiles of the same frame run in this launch (k_fused_rows_taa): the
+// accumulated colour and reprojected positions they read are stored
+// device-coherent and the block publishes done[...] = epoch once they are
+// (the hand-off of bmfr_taa_tile.h wait_k1_blocks).
+template <int NS, int FS, class IN, bool COH = false>
+__device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K1Lds<NS + FS + 3>& L, int g) {
     constexpr int B = NS + FS + 3;
-    __shared__ K1Lds<B> L;
     const int t = threadIdx.x;
-    const int g = xcd_swizzle(blockIdx.x, gridDim.x);
     const int frame = A.frame;
     const NoisyInputs& in = A.in;
     // Diagnostic build only (-DBMFR_STAMPS): per-block phase timestamps.
@@ -302,6 +308,12 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
     BMFR_STAMP(0);
     int bx, by;
     k1_block(P, g, bx, by);
+    if constexpr (COH) {
+        if (t == 0) {
+            L.flag = (by - P.by0) * P.nbx + (bx - P.bx0);  // this block's completion flag
+            L.delay = P.debug_delay;
+        }
+    }
 
     // ---- accumulate_noisy_data (bmfr.cl:310-484) for rows t + 256s ----
     FloatRows<B, kSubs> M;
@@ -330,7 +342,8 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
         if (it.owner) {
             st3(A.noisy_out, it.lin, it.color);
             st_px(A.spp_out, it.lin, it.spp);
-            st_px(A.prev_pixel_out, it.lin, make_float2(it.pfx, it.pfy));
+            if constexpr (COH) st2_coh(coh_plane(A.prev_pixel_out), it.lin, make_float2(it.pfx, it.pfy));
+            else st_px(A.prev_pixel_out, it.lin, make_float2(it.pfx, it.pfy));
         }
     }
     report_reach(P, A.reach, over);
@@ -428,7 +441,8 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
             c.z = c.z < 0.f ? 0.f : c.z;
             const f3 acc = blend_filtered(P, c, pp[s].x, pp[s].y, (uint8_t)((bits[s] >> 1) & 15u),
                                           (uint8_t)(bits[s] >> 8), A.acc_prev, frame);
-            st3(A.acc_out, lin[s], acc);
+            if constexpr (COH) st3_coh(coh_plane(A.acc_out), lin[s], acc);
+            else st3(A.acc_out, lin[s], acc);
         }
     }
 #ifdef BMFR_STAMPS
@@ -436,6 +450,34 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
 #endif
     BMFR_STAMP(5);
 #undef BMFR_STAMP
+    if constexpr (COH) {  // as k1_cols_body: stores performed, then the flag
+        const int delay = L.delay;
+        if (delay > 0 && g % kDelayStride == kDelayPhase)  // diagnostics: tiles really wait
+            for (int k = 0; k < delay; ++k) __builtin_amdgcn_s_sleep(127);
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+        __syncthreads();
+        if (t == 0) __hip_atomic_store(&A.done[L.flag], A.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <int NS, int FS, class IN>
+__global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
+    __shared__ K1Lds<NS + FS + 3> L;
+    k1_rows_body<NS, FS, IN>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
+}
+
+// The one-launch frame with this K1 (f32 tmp_data): K1 blocks, then the
+// frame's TAA tiles waiting on their completion flags (as k_fused_cols_taa,
+// bmfr_fused_cols.hip).
+template <int NS, int FS, class IN>
+__global__ __launch_bounds__(kThreads) void k_fused_rows_taa(Params P, K1Args A, TaaArgs T, int nk1, int nk1p) {
+    __shared__ union {
+        K1Lds<NS + FS + 3> k1;
+        FrameTaaLds k2;
+    } U;
+    const int b = blockIdx.x;
+    if (b < nk1) k1_rows_body<NS, FS, IN, true>(P, A, U.k1, xcd_swizzle(b, nk1));
+    else if (b >= nk1p) frame_taa_part<IN, true>(P, T, b, nk1p, U.k2);
 }
 
 bool fused_supported(const Params& P) {
@@ -448,6 +490,19 @@ bool fused_supported(const Params& P) {
 template <int FS, class IN>
 static void launch_k1(const Params& P, hipStream_t st, const FusedArgs& A) {
     hipLaunchKernelGGL((k_fused<4, FS, IN>), dim3(k1_blocks(P)), dim3(kThreads), 0, st, P, k1_args(A));
+}
+
+template <int FS, class IN>
+static void launch_rows_frame(const Params& P, hipStream_t st, const FusedArgs& A) {
+    const int nk1 = P.ring < 0 || P.nbx <= 0 || P.nby <= 0 ? 0 : k1_blocks(P), nk1p = (nk1 + 7) & ~7;
+    hipLaunchKernelGGL((k_fused_rows_taa<4, FS, IN>), dim3(nk1p + frame_taa_tiles(P)), dim3(kThreads), 0, st, P,
+                       k1_args(A), taa_args(A), nk1, nk1p);
+}
+
+hipError_t launch_fused_rows_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
+    if (P.scaled == 6) P.input_half ? launch_rows_frame<6, _Float16>(P, st, A) : launch_rows_frame<6, float>(P, st, A);
+    else P.input_half ? launch_rows_frame<9, _Float16>(P, st, A) : launch_rows_frame<9, float>(P, st, A);
+    return hipGetLastError();
 }
 
 hipError_t launch_fused_k1(const Params& P, hipStream_t st, const FusedArgs& A) {

@@ -43,19 +43,33 @@ constexpr int kPre = 2;          // step-0 noise columns per wave prefetched in 
 // pivot through an LDS flag instead of a barrier per column, so a buffer is
 // reused only once every wave has finished the step that read it.
 constexpr int kUBufs = 3;
+// Phase 1 -> 3, per thread: the previous accumulated filtered colour of its
+// four items (12 floats).  Where the matrix area has room beside the u
+// buffers (B >= 16) they wait in registers until the fit has loaded its
+// columns and then go there, so the work-group's LDS stays within 40 KB (four
+// work-groups per CU); otherwise they have their own LDS array.
+constexpr int kKeep = 4 * 3 * kThreads;
+constexpr bool keep_in_m(int B) {
+    return (B - 1) * 64 * kSlots * 2 >= (kUBufs * 64 * kUStride + kKeep) * 4;
+}
 template <int B>
 struct Lds {
     union {
         _Float16 M[B - 1][64 * kSlots];  // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
-        float u[kUBufs][64 * kUStride];  // Householder vectors, u_c in buffer c % kUBufs
+        struct {
+            float u[kUBufs][64 * kUStride];  // Householder vectors, u_c in buffer c % kUBufs
+            float keep_m[keep_in_m(B) ? kKeep : 1];
+        };
     };
-    float keep[4][3][kThreads];  // phase 1 -> 3: previous accumulated filtered colour per item
+    float keep_s[keep_in_m(B) ? 1 : kKeep];
+    __device__ float* keep() { return keep_in_m(B) ? keep_m : keep_s; }  // [(item * 3 + ch) * kThreads + t]
     float piv[kUBufs][2];               // |u|^2 and RN(1/|u|^2) of the published vector
     int pub;                            // highest published pivot column
     int prog[4];                        // per wave: the last step it has applied
     int timeout;                        // a flag wait of this block gave up (reported once, at the end)
     int max_polls;                      // Params::max_polls (kept here: read only once a flag is not ready)
     int delay;                          // Params::debug_delay (diagnostics, read at the block's end)
+    int flag;                           // one-launch frame: index of this block's completion flag
     float R[(B - 2) * (B - 2) * 3];     // R[x][y][ch], x = column (as k_fused)
     float weights[(B - 3) * 3];
     float mm[3 * (B - 3)];              // per scaled feature: min, max, 1/(max-min)
@@ -318,6 +332,9 @@ struct WaveFit {
     static __device__ __forceinline__ bool owns(int W, int c) { return c >= 1 && c < B && ((c - 1) & 3) == W; }
     static constexpr int owner(int c) { return (c - 1) & 3; }
     static constexpr int slot(int c) { return (c - 1) >> 2; }
+    // Step-0 noise columns prefetched per wave: none at B = 16, where the
+    // fit's registers are the limit for four work-groups per CU.
+    static constexpr int NP = B >= 16 ? 0 : kPre;
 
     // The first column a wave updates at step 0: a feature column for every wave.
     static __device__ __forceinline__ int first_column(int W) { return 1 + W; }
@@ -331,15 +348,15 @@ struct WaveFit {
         const bool publish = nxt < NF && W == owner(nxt);
         if constexpr (c == 0) {
             if (publish) {  // column 1 of wave 0: its first column
-                update_column0(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre[0], true, noise2);
+                update_column0(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre[0], NP > 0, noise2);
                 publish_pivot<nxt, B>(a[slot(nxt)], L, l);
             }
             sfor<NSL>([&](auto K) {
                 constexpr int k = decltype(K)::value;
                 const int fb = 1 + W + 4 * k;
-                if (owns(W, fb) && !(publish && fb == nxt))  // slots < kPre: feature columns, prefetched
+                if (owns(W, fb) && !(publish && fb == nxt))  // slots < NP: feature columns, prefetched
                     update_column0(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr,
-                                   pre[k < kPre ? k : 0], k < kPre, noise2);
+                                   pre[k < kPre ? k : 0], k < NP, noise2);
             });
         } else {
             if (1 + W + 4 * ((B - 2 - W) / 4) > c) {  // this wave's last column is past the pivot
@@ -389,7 +406,7 @@ struct WaveFit {
     static __device__ __forceinline__ void prefetch_noise(int W, int l, const float* __restrict__ noise,
                                                           float (&pre)[kPre][kSlots]) {
 #pragma unroll
-        for (int k = 0; k < kPre; ++k) {
+        for (int k = 0; k < NP; ++k) {
             const float* src = noise + (first_column(W) + 4 * k - 1) * kBlockPixels + l;
 #pragma unroll
             for (int j = 0; j < kSlots; ++j) pre[k][j] = src[64 * j];
@@ -397,7 +414,8 @@ struct WaveFit {
     }
 
     static __device__ __forceinline__ void run(Lds<B>& L, int W, int l, const float* __restrict__ noise,
-                                               const float (&pre)[kPre][kSlots], double noise2, int mp) {
+                                               const float (&pre)[kPre][kSlots], double noise2, int mp,
+                                               const float (&kp)[4][3]) {
         h2 a[NSL][8];
         sfor<NSL>([&](auto K) {
             constexpr int k = decltype(K)::value;
@@ -417,6 +435,13 @@ struct WaveFit {
             else L.prog[l - 1] = -1;
         }
         k1_barrier();  // the u buffers alias M
+        if constexpr (keep_in_m(B)) {  // phase 1's kept colours into the matrix area beside the u buffers
+            const int t = W * 64 + l;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) L.keep_m[(i * 3 + ch) * kThreads + t] = kp[i][ch];
+        }
 
         // Scale the position features to the block's [min, max] (bmfr.cl:510-542).
         sfor<NSL>([&](auto K) {
@@ -550,6 +575,11 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 #endif
     int bx, by;
     k1_block(P, g, bx, by);
+    // COH: this block's completion flag, in the launch's block rectangle (g
+    // itself unless the launch is a tiled context's border ring); parked in
+    // LDS until the end (fewer scalar registers live across the kernel)
+    if constexpr (COH)
+        if (t == 0) L.flag = (by - P.by0) * P.nbx + (bx - P.bx0);
     const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
 
     // ---- accumulate_noisy_data (bmfr.cl:310-484), rows l + 64 (4w + i) ----
@@ -562,6 +592,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // Software-pipelined one item deep: item i + 1's current-frame loads go
     // out right behind item i's reprojection taps, so each wait for taps
     // leaves the next item's loads in flight.
+    float kp[4][3];  // keep_in_m(B): the kept colours, in registers until the fit has loaded M
     NoisyCur<IN> cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly, frame);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -584,9 +615,15 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
             spps |= (uint32_t)it.spp << (8 * i);
             ibits |= ((uint32_t)it.owner << i) | ((uint32_t)it.prev_f_divided << (4 + i));
             over = max(over, it.over);
-            L.keep[i][0][t] = it.prev_f.x;
-            L.keep[i][1][t] = it.prev_f.y;
-            L.keep[i][2][t] = it.prev_f.z;
+            if constexpr (keep_in_m(B)) {
+                kp[i][0] = it.prev_f.x;
+                kp[i][1] = it.prev_f.y;
+                kp[i][2] = it.prev_f.z;
+            } else {
+                L.keep_s[(i * 3 + 0) * kThreads + t] = it.prev_f.x;
+                L.keep_s[(i * 3 + 1) * kThreads + t] = it.prev_f.y;
+                L.keep_s[(i * 3 + 2) * kThreads + t] = it.prev_f.z;
+            }
             if (it.owner) {
                 st3(A.noisy_out, it.lin, it.color);
                 st_px(A.spp_out, it.lin, it.spp);
@@ -612,7 +649,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 
     // ---- fit: min/max scaling, Householder QR, right-hand side ----
     if (t == 0) L.delay = P.debug_delay;  // read after the fit's barriers
-    WaveFit<NS, FS>::run(L, w, l, A.noise, pre, P.noise2, P.max_polls);
+    WaveFit<NS, FS>::run(L, w, l, A.noise, pre, P.noise2, P.max_polls, kp);
     // Phase 3's loads (normal and position of the four items, bmfr.cl:725-729)
     // go out now: they land while wave 0 back-substitutes and the others wait.
     int l3 = l;  // opaque copy: recompute phase-1 addresses instead of keeping them live across the fit
@@ -646,38 +683,53 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     }
 
     // ---- weighted_sum (bmfr.cl:717-750) + temporal blend (bmfr.cl:778-849) ----
-    // Features outer, items inner: each weight / min-max is live for one
-    // feature only.  Items (0, 1) and (2, 3) as packed f32 pairs: every lane
-    // rounds as upstream's scalar sequence, each item in feature order.
+    // Items (0, 1) and (2, 3) as packed f32 pairs: every lane rounds as
+    // upstream's scalar sequence, each item in feature order.
     f2v cp[2][3];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
         for (int ch = 0; ch < 3; ++ch) cp[h][ch] = f2v{0.f, 0.f};
+    // Item pairs outer where it saves registers: one pair's positions, powers
+    // and sums live at a time (features outer kept every item's in registers:
+    // 10 VGPRs of spills in the K1-only kernel at B = 13, 36-67 at B = 16
+    // with four work-groups per CU; pairs outer: none).  Features outer for
+    // the one-launch frame at B = 13, which has no spills either way and
+    // runs ~1 % faster so (each weight and min / max loaded once).
+#ifdef PAIRS_ALL
+    constexpr bool kPairs = true;
+#else
+    constexpr bool kPairs = B >= 16 || !COH;
+#endif
+    constexpr int NH = kPairs ? 2 : 1;
 #pragma unroll
-    for (int f = 0; f < B - 3; ++f) {
-        const f2v wv[3] = {f2v{L.weights[3 * f], L.weights[3 * f]}, f2v{L.weights[3 * f + 1], L.weights[3 * f + 1]},
-                           f2v{L.weights[3 * f + 2], L.weights[3 * f + 2]}};
-        float bmin = 0.f, d = 0.f, rcp = 0.f;
-        if (f >= NS) {
-            bmin = L.mm[3 * (f - NS)];
-            d = L.mm[3 * (f - NS) + 1] - bmin;
-            rcp = L.mm[3 * (f - NS) + 2];
-        }
+    for (int hh = 0; hh < NH; ++hh) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            f2v v = {feature_value(f, nrm[2 * h], wp[2 * h]), feature_value(f, nrm[2 * h + 1], wp[2 * h + 1])};
+        for (int f = 0; f < B - 3; ++f) {
+            const f2v wv[3] = {f2v{L.weights[3 * f], L.weights[3 * f]},
+                               f2v{L.weights[3 * f + 1], L.weights[3 * f + 1]},
+                               f2v{L.weights[3 * f + 2], L.weights[3 * f + 2]}};
+            float bmin = 0.f, d = 0.f, rcp = 0.f;
             if (f >= NS) {
-                v = v - f2v{bmin, bmin};
-                if (fabsf(d) > 1.0f) {
-                    const f2v q0 = v * f2v{rcp, rcp};
-                    const f2v r = __builtin_elementwise_fma(-q0, f2v{d, d}, v);
-                    v = __builtin_elementwise_fma(r, f2v{rcp, rcp}, q0);
-                }
+                bmin = L.mm[3 * (f - NS)];
+                d = L.mm[3 * (f - NS) + 1] - bmin;
+                rcp = L.mm[3 * (f - NS) + 2];
             }
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) cp[h][ch] = cp[h][ch] + wv[ch] * v;
+            for (int h = kPairs ? hh : 0; h < (kPairs ? hh + 1 : 2); ++h) {
+                f2v v = {feature_value(f, nrm[2 * h], wp[2 * h]), feature_value(f, nrm[2 * h + 1], wp[2 * h + 1])};
+                if (f >= NS) {
+                    v = v - f2v{bmin, bmin};
+                    if (fabsf(d) > 1.0f) {
+                        const f2v q0 = v * f2v{rcp, rcp};
+                        const f2v r = __builtin_elementwise_fma(-q0, f2v{d, d}, v);
+                        v = __builtin_elementwise_fma(r, f2v{rcp, rcp}, q0);
+                    }
+                }
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) cp[h][ch] = cp[h][ch] + wv[ch] * v;
+            }
+            __builtin_amdgcn_sched_barrier(0);  // one feature's weights live at a time
         }
-        __builtin_amdgcn_sched_barrier(0);  // one feature's weights live at a time
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -692,7 +744,8 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                                     : 1.f;
             const float beta = 1.f - alpha;
             const int t3 = l3 + 64 * w;
-            const f3 prev{L.keep[i][0][t3], L.keep[i][1][t3], L.keep[i][2][t3]};
+            const float* kb = L.keep();
+            const f3 prev{kb[(i * 3) * kThreads + t3], kb[(i * 3 + 1) * kThreads + t3], kb[(i * 3 + 2) * kThreads + t3]};
             const f3 acc{alpha * ci.x + beta * prev.x, alpha * ci.y + beta * prev.y, alpha * ci.z + beta * prev.z};
             if constexpr (COH) st3_coh(coh_plane(A.acc_out), lin[i], acc);
             else st3(A.acc_out, lin[i], acc);
@@ -713,7 +766,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's stores are performed
         lds_barrier();                       // ... and every wave's
         if (t == 0)
-            __hip_atomic_store(&A.done[g], A.epoch | (L.timeout ? kDoneTimeout : 0u), __ATOMIC_RELAXED,
+            __hip_atomic_store(&A.done[L.flag], A.epoch | (L.timeout ? kDoneTimeout : 0u), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -724,7 +777,7 @@ __global__ __launch_bounds__(kThreads, kColsWaves) void k_fused_cols(Params P, K
     k1_cols_body<NS, FS, IN>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
 }
 
-// K1 and K2 (64 x kSeqTaaH tiles) in one launch: work-groups [0, nk1) are K1
+// K1 and K2 (64 x kFrameTaaH tiles) in one launch: work-groups [0, nk1) are K1
 // blocks, [nk1p, nk1p + nk2) TAA tiles (nk1p = nk1 rounded up to the 8 XCDs;
 // the ones between exit).  The in-order dispatch runs the tiles in K1's
 // tail, where its last work-groups leave CUs idle, and a frame costs one
@@ -737,28 +790,16 @@ __global__ __launch_bounds__(kThreads, kColsWaves) void k_fused_cols(Params P, K
 //     their outputs device-coherent.  Work-groups of one XCD are dispatched
 //     in order, so every K1 block a waiting tile needs has been dispatched:
 //     the waits end.
-constexpr int kSeqTaaH = 12;
 template <int NS, int FS, class IN, bool SAME = false>
 __global__ __launch_bounds__(kThreads, 4) void k_fused_cols_taa(Params P, K1Args A, Params P2, TaaArgs T, int nk1,
                                                                 int nk1p) {
-    constexpr int HW = 64 + 2, N = HW * (kSeqTaaH + 2);
     __shared__ union {
         Lds<NS + FS + 3> k1;
-        struct {
-            float4 Y[N];
-            double sE[kPowrENum];
-            double2 sRP[kPowrRPNum];
-        } k2;
+        FrameTaaLds k2;
     } U;
     const int b = blockIdx.x;
-    if (b < nk1) {
-        k1_cols_body<NS, FS, IN, SAME>(P, A, U.k1, xcd_swizzle(b, nk1));
-    } else if (b >= nk1p) {
-        const int gx = (P2.tx1 - P2.tx0 + 63) / 64, n2 = (int)gridDim.x - nk1p;
-        const int gi = xcd_swizzle(b - nk1p, n2);
-        taa_tile<IN, kSeqTaaH, SAME>(P2, T, P2.tx0 + (gi % gx) * 64, P2.ty0 + (gi / gx) * kSeqTaaH, U.k2.Y,
-                                     U.k2.sE, U.k2.sRP);
-    }
+    if (b < nk1) k1_cols_body<NS, FS, IN, SAME>(P, A, U.k1, xcd_swizzle(b, nk1));
+    else if (b >= nk1p) frame_taa_part<IN, SAME>(P2, T, b, nk1p, U.k2);
 }
 
 }  // namespace cols
@@ -772,18 +813,21 @@ static void launch_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
 }
 
 bool seq_fused_supported(const Params& P) { return fused_cols_supported(P) && P.ring == 0; }
-// (untiled: a tiled context's K2 also forwards the reach report, k_fused_taa)
-bool frame_fused_supported(const Params& P) { return seq_fused_supported(P) && !P.check_reach; }
+// Untiled frames, a tiled context's whole frame and its border launch (the
+// ring of K1 blocks + the tile's TAA; the last work-group forwards the reach
+// report).
+bool frame_fused_supported(const Params& P) { return fused_supported(P); }
 
 template <int FS, class IN>
 static void launch_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
-    const int nk1 = k1_blocks(P), nk1p = (nk1 + 7) & ~7;
-    const int nk2 = ((P.tx1 - P.tx0 + 63) / 64) * ((P.ty1 - P.ty0 + cols::kSeqTaaH - 1) / cols::kSeqTaaH);
+    const int nk1 = P.ring < 0 || P.nbx <= 0 || P.nby <= 0 ? 0 : k1_blocks(P), nk1p = (nk1 + 7) & ~7;
+    const int nk2 = frame_taa_tiles(P);
     hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN, true>), dim3(nk1p + nk2), dim3(cols::kThreads), 0, st, P,
                        k1_args(A), P, taa_args(A), nk1, nk1p);
 }
 
 hipError_t launch_fused_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
+    if (!fused_cols_supported(P)) return launch_fused_rows_frame_one(P, st, A);  // f32 tmp_data
     if (P.scaled == 6) P.input_half ? launch_frame_one<6, _Float16>(P, st, A) : launch_frame_one<6, float>(P, st, A);
     else P.input_half ? launch_frame_one<9, _Float16>(P, st, A) : launch_frame_one<9, float>(P, st, A);
     return hipGetLastError();
@@ -793,7 +837,7 @@ template <int FS, class IN>
 static void launch_cols_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
                             const FusedArgs* A2) {
     const int nk1 = A ? k1_blocks(P) : 0, nk1p = (nk1 + 7) & ~7;
-    const int nk2 = A2 ? ((P2.tx1 - P2.tx0 + 63) / 64) * ((P2.ty1 - P2.ty0 + cols::kSeqTaaH - 1) / cols::kSeqTaaH) : 0;
+    const int nk2 = A2 ? frame_taa_tiles(P2) : 0;
     if (nk1 + nk2 == 0) return;
     const TaaArgs T = A2 ? taa_args(*A2) : TaaArgs{};
     hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN>), dim3(nk2 ? nk1p + nk2 : nk1), dim3(cols::kThreads), 0,

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, TaaArgs T) {
     // one-pixel halo lies inside the buffer region).
     const int gi = xcd_swizzle(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int bxi = gi % gridDim.x, byi = gi / gridDim.x;
-    forward_reach(T);
+    forward_reach(T, blockIdx.x == 0 && blockIdx.y == 0);
     taa_tile<IN, kTaaH>(P, T, P.tx0 + bxi * kTaaW, P.ty0 + byi * kTaaH, Y, sE, sRP);
 }
 

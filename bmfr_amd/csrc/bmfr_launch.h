@@ -106,11 +106,13 @@ hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedAr
 // Sequence kernel (bmfr_process_sequence): K1 of a frame (A, or none) and K2
 // of the frame before it (A2, or none) in one launch.
 bool seq_fused_supported(const Params& P);
-// One-launch frame (bmfr_process_frame, untiled): K1 blocks, then the TAA
-// tiles of the same frame, each waiting on the completion flags of the K1
-// blocks under its footprint.
+// One-launch frame (bmfr_process_frame; a tiled context's border part): K1
+// blocks, then the TAA tiles of the same frame, each waiting on the
+// completion flags of the K1 blocks under its footprint.
 bool frame_fused_supported(const Params& P);
 hipError_t launch_fused_frame_one(const Params& P, hipStream_t st, const FusedArgs& A);
+// The same with the row-split K1 (f32 tmp_data, bmfr_fused.hip).
+hipError_t launch_fused_rows_frame_one(const Params& P, hipStream_t st, const FusedArgs& A);
 hipError_t launch_fused_k1_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
                                const FusedArgs* A2);
 hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A);

@@ -70,36 +70,60 @@ __device__ __forceinline__ void report_sync_timeout(unsigned* err, int which, in
 // cache line a tile loads may straddle a neighbouring block that has not
 // finished; the tile never uses those bytes, and any later read of them in
 // the launch is again an SC1 load that does not hit a stale copy.
+// One completion flag (bounded poll, one lane).
+__device__ __forceinline__ void wait_done(const Params& P, const TaaArgs& T, const unsigned* f) {
+    const int limit = 4 * P.max_polls;
+    for (int k = 0;; ++k) {
+        const unsigned v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v & ~kDoneTimeout) >= T.epoch) {
+            if (v & kDoneTimeout) report_sync_timeout(T.sync_err, kSyncPivot, T.frame);
+            return;
+        }
+        if (k >= limit) {
+            report_sync_timeout(T.sync_err, kSyncTile, T.frame);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// K1 block (bx, by) of launch P runs in this launch (a tiled context's border
+// launch holds only the ring outside [rx0, rx1) x [ry0, ry1), none when
+// ring < 0; the interior blocks ran in the launch before, complete before
+// this one starts).
+__device__ __forceinline__ bool k1_in_launch(const Params& P, int bx, int by) {
+    if (P.ring <= 0) return P.ring == 0;
+    return bx < P.rx0 || bx >= P.rx1 || by < P.ry0 || by >= P.ry1;
+}
+
 __device__ __forceinline__ void wait_k1_blocks(const Params& P, const TaaArgs& T, int x0, int y0, int th) {
     const int2 off = kBlockOffsets[T.frame & 15];
-    const int xa = max(x0 - 1, P.ox), xb = min(x0 + 64, P.ox + P.stride - 1);
-    const int ya = max(y0 - 1, P.oy), yb = min(y0 + th, P.oy + P.rows - 1);
+    // the tile and its 1-px halo, inside the output rectangle + 1 px (a tiled
+    // context's K1 blocks cover exactly that) and the buffer region
+    const int xa = max(x0 - 1, P.ox), xb = min(min(x0 + 64, P.tx1), P.ox + P.stride - 1);
+    const int ya = max(y0 - 1, P.oy), yb = min(min(y0 + th, P.ty1), P.oy + P.rows - 1);
     const int bxa = (xa + kEdge / 2 - off.x) / kEdge, bxb = (xb + kEdge / 2 - off.x) / kEdge;
     const int bya = (ya + kEdge / 2 - off.y) / kEdge, byb = (yb + kEdge / 2 - off.y) / kEdge;
     const int nx = bxb - bxa + 1, n = nx * (byb - bya + 1);
     const int t = threadIdx.x;
     if (t < n) {
         const int bx = bxa + t % nx, by = bya + t / nx;
-        const unsigned* f = T.done + (by - P.by0) * P.nbx + (bx - P.bx0);
-        const int limit = 4 * P.max_polls;
-        for (int k = 0;; ++k) {
-            const unsigned v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((v & ~kDoneTimeout) >= T.epoch) {
-                if (v & kDoneTimeout) report_sync_timeout(T.sync_err, kSyncPivot, T.frame);
-                break;
-            }
-            if (k >= limit) {
-                report_sync_timeout(T.sync_err, kSyncTile, T.frame);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
+        if (k1_in_launch(P, bx, by)) wait_done(P, T, T.done + (by - P.by0) * P.nbx + (bx - P.bx0));
     }
     __syncthreads();
 }
 
-__device__ __forceinline__ void forward_reach(const TaaArgs& T) {
-    if (T.reach_dev && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+// Every K1 block of this launch has published (the reach report is complete).
+__device__ __forceinline__ void wait_all_k1_blocks(const Params& P, const TaaArgs& T) {
+    for (int i = threadIdx.x; i < P.nbx * P.nby; i += blockDim.x) {
+        const int bx = P.bx0 + i % P.nbx, by = P.by0 + i / P.nbx;
+        if (k1_in_launch(P, bx, by)) wait_done(P, T, T.done + i);
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void forward_reach(const TaaArgs& T, bool here = true) {
+    if (T.reach_dev && here && threadIdx.x == 0) {
         const unsigned v = atomicExch(T.reach_dev, 0u);
         volatile unsigned* h = T.reach_host;
         if (v > h[0]) h[0] = v;
@@ -188,6 +212,34 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
             st3(T.result, pix(P, x, y), r);
         }
     }
+}
+
+// The TAA part of a one-launch frame kernel (K1 blocks, then the frame's
+// TAA tiles; bmfr_fused_cols.hip k_fused_cols_taa, bmfr_fused.hip
+// k_fused_rows_taa): work-group b >= nk1p of the launch is tile b - nk1p
+// (64 x TH, XCD-aware order).  COH: the tiles wait for the K1 blocks of the
+// same launch; a tiled context's last work-group then forwards the reach
+// report once every K1 block of the launch has raised it.
+constexpr int kFrameTaaH = 12;
+struct FrameTaaLds {
+    float4 Y[(64 + 2) * (kFrameTaaH + 2)];
+    double sE[kPowrENum];
+    double2 sRP[kPowrRPNum];
+};
+template <class IN, bool COH>
+__device__ __forceinline__ void frame_taa_part(const Params& P2, const TaaArgs& T, int b, int nk1p, FrameTaaLds& L) {
+    const int gx = (P2.tx1 - P2.tx0 + 63) / 64, n2 = (int)gridDim.x - nk1p;
+    const int gi = xcd_swizzle(b - nk1p, n2);
+    taa_tile<IN, kFrameTaaH, COH>(P2, T, P2.tx0 + (gi % gx) * 64, P2.ty0 + (gi / gx) * kFrameTaaH, L.Y, L.sE, L.sRP);
+    if constexpr (COH) {
+        if (T.reach_dev && b == (int)gridDim.x - 1) {
+            wait_all_k1_blocks(P2, T);
+            forward_reach(T);
+        }
+    }
+}
+inline int frame_taa_tiles(const Params& P) {
+    return ((P.tx1 - P.tx0 + 63) / 64) * ((P.ty1 - P.ty0 + kFrameTaaH - 1) / kFrameTaaH);
 }
 
 }  // namespace bmfr

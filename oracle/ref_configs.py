@@ -141,6 +141,8 @@ FULL_REF_CONFIGS = {
         RefConfig("f3840x2160_f13", 3840, 2160, half_tmp=0, frames=17),  # config 3, fp32 tmp_data
         RefConfig("f3840x2160_h16", 3840, 2160, scaled=SCALED_THIRD_ORDER, frames=17),  # config 5 (3rd order)
         RefConfig("f7680x4320_h13", 7680, 4320, frames=3),               # config 4's frame, untiled
+        # B = 16 with f32 tmp_data: the MFMA experiment's tolerance reference (tools/mfma_experiment.py)
+        RefConfig("f3840x2160_f16", 3840, 2160, scaled=SCALED_THIRD_ORDER, half_tmp=0, frames=4),
         RefConfig("f1280x720_h13", 1280, 720, frames=60),                # a whole 60-frame sequence
     )
 }

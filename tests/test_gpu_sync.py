@@ -59,9 +59,8 @@ def test_exhausted_waits_report_sync_timeout(half_tmp, gpu):
     frames = _frames(W, H, 3)
     den.debug_sync(max_polls=0)
     _run(den, frames[:2])
-    if not half_tmp:  # the f32-tmp_data K1 has no flag waits (work-group barriers only)
-        assert den.frame_status() == 0
-        return
+    # half tmp_data: K1's pivot waits and the tiles' waits; f32 (row-split K1,
+    # work-group barriers): the tiles' waits of the one-launch frame
     assert den.frame_status() == _lib.SYNC_TIMEOUT
     with pytest.raises(bmfr_amd.BmfrError) as e:
         _run(den, frames[2:3], first=2)
@@ -83,17 +82,18 @@ def test_sequence_api_reports_sync_timeout(gpu):
     assert den.frame_status() == 0
 
 
-@pytest.mark.parametrize("W,H", [(3840, 2160), (1920, 1080)])
-def test_delayed_k1_blocks_one_launch_exact(W, H, gpu):
+@pytest.mark.parametrize("W,H,half_tmp", [(3840, 2160, 1), (1920, 1080, 1), (3840, 2160, 0)])
+def test_delayed_k1_blocks_one_launch_exact(W, H, half_tmp, gpu):
     """One K1 block in 61 sleeps ~0.3 ms before it raises its completion
     flag, so the TAA tiles over it really wait on the flags: the one-launch
     frame must still equal the two-launch frame (profiling on: K1 and K2 as
     separate launches, no flags) bit for bit on the output and every state
     plane, and report no timeout."""
     frames = _frames(W, H, 4)
-    one = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, use_half_precision_in_tmp_data=half_tmp)
+    one = bmfr_amd.Denoiser(cfg)
     one.debug_sync(k1_delay=40)
-    two = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    two = bmfr_amd.Denoiser(cfg)
     two.set_profiling(True, capacity=16)
     for i, fr in enumerate(frames):
         _run(one, [fr], first=i)

@@ -3,15 +3,16 @@
 section 4).  Runs on the GPU box.
 
 The f32-tmp_data stage pipeline (StagePipeline, library_powr = 1) is run on
-the synthetic 3840x2160 sequence twice: once with libbmfr's exact VALU fitter
-(bmfr_fitter), once with the compact-WY fitter of tools/wy_fitter.hip whose
+the synthetic 3840x2160 sequence with libbmfr's exact VALU fitter
+(bmfr_fitter) and with the compact-WY fitter of tools/wy_fitter.hip whose
 trailing-panel update runs on MFMA (tools/libwy.so; build:
-hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/wy_fitter.hip -o tools/libwy.so).
+hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/wy_fitter.hip -o tools/libwy.so)
+at each panel width NB (4, 8, 16 = the whole QR as one panel).
 Reported: each fitter's kernel time on the same tmp_data (HIP events,
 median of 10), the fused f32 K1 for context, and the TAA output's relative L2
 to the reference kernels' default build (contraction on) and strict build.
 
-  python tools/mfma_experiment.py [W H FRAMES]
+  python tools/mfma_experiment.py [W H FRAMES [B [NB,...]]]   (B = 13 or 16)
 """
 import ctypes as C
 import json
@@ -32,10 +33,14 @@ from bmfr_amd.pipeline import _ptr  # noqa: E402
 from ref_configs import FULL_REF_CONFIGS  # noqa: E402
 
 W, H, FR = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (3840, 2160, 4)))
-rc = FULL_REF_CONFIGS["f3840x2160_f13"] if (W, H) == (3840, 2160) else None
+BC = int(sys.argv[4]) if len(sys.argv) > 4 else 13
+NBS = [int(x) for x in sys.argv[5].split(",")] if len(sys.argv) > 5 else [4, 8, 16]
+rc = FULL_REF_CONFIGS.get(f"f{W}x{H}_f{BC}")
 wy = C.CDLL(os.path.join(ROOT, "tools", "libwy.so"))
-wy.wy_fitter.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_void_p]
-cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, use_half_precision_in_tmp_data=0, library_powr=1)
+wy.wy_fitter.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_void_p, C.c_int,
+                         C.c_int]
+cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, use_half_precision_in_tmp_data=0, library_powr=1,
+                          scaled=bmfr_amd.SCALED_THIRD_ORDER if BC == 16 else bmfr_amd.SCALED_DEFAULT)
 
 
 def run_stages(sp, vp, jit, f, fitter):
@@ -60,11 +65,13 @@ def valu_fitter(sp, f):
                              _ptr(sp.mins_maxs), _ptr(sp.tmp_data), f), "fitter")
 
 
-def wy_fitter(sp, f):
-    G = sp.sizes.blocks
-    err = wy.wy_fitter(G, _ptr(sp.tmp_data), _ptr(sp.weights), _ptr(sp.mins_maxs), f, cfg.noise_amount * 2.0,
-                       torch.cuda.current_stream().cuda_stream)
-    assert err == 0, err
+def wy_fitter_nb(nb):
+    def fit(sp, f):
+        G = sp.sizes.blocks
+        err = wy.wy_fitter(G, _ptr(sp.tmp_data), _ptr(sp.weights), _ptr(sp.mins_maxs), f, cfg.noise_amount * 2.0,
+                           torch.cuda.current_stream().cuda_stream, BC, nb)
+        assert err == 0, err
+    return fit
 
 
 def rel_l2(a, b):
@@ -84,14 +91,15 @@ def time_ms(fn, reps=10):
     return float(np.median(out))
 
 
-exact, blocked = bmfr_amd.StagePipeline(cfg), bmfr_amd.StagePipeline(cfg)
+exact = bmfr_amd.StagePipeline(cfg)
+blocked = {nb: bmfr_amd.StagePipeline(cfg) for nb in NBS}
 refs = {m: ref_run.RefLoop(rc, m) for m in ("strict", "default")} if rc and ref_run.available(rc.name) else {}
-res = {"image": f"{W}x{H}", "buffer_count": 13, "tmp_data": "f32", "frames": []}
+res = {"image": f"{W}x{H}", "buffer_count": BC, "tmp_data": "f32", "panel_widths": NBS, "frames": []}
 for f in range(FR):
     fr = bmfr_amd.synth_frame_device(W, H, f)
     vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
     _, jit = bmfr_amd.synth_camera(W, H, f)
-    for sp, fit in ((exact, valu_fitter), (blocked, wy_fitter)):
+    for sp, fit in [(exact, valu_fitter)] + [(blocked[nb], wy_fitter_nb(nb)) for nb in NBS]:
         sp.upload(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"])
         run_stages(sp, vp, jit, f, fit)
     row = {"frame": f}
@@ -100,12 +108,14 @@ for f in range(FR):
         rl.upload(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"])
         rl.run_stages(vp, jit, f, record=rec)
         rl.swap()
-        row[f"wy_vs_ref_{m}"] = rel_l2(blocked.cur(blocked.result), rec["result"])
         row[f"valu_vs_ref_{m}"] = rel_l2(exact.cur(exact.result), rec["result"])
-    row["wy_vs_valu"] = rel_l2(blocked.cur(blocked.result), exact.cur(exact.result))
+        for nb in NBS:
+            row[f"wy{nb}_vs_ref_{m}"] = rel_l2(blocked[nb].cur(blocked[nb].result), rec["result"])
+    for nb in NBS:
+        row[f"wy{nb}_vs_valu"] = rel_l2(blocked[nb].cur(blocked[nb].result), exact.cur(exact.result))
     res["frames"].append(row)
     print(json.dumps(row), flush=True)
-    if f == FR - 1:  # both fitters on the same tmp_data of this frame's stage 1
+    if f == FR - 1:  # every fitter on the same tmp_data of this frame's stage 1
         saved = exact.tmp_data.clone()
 
         def again(fn):
@@ -114,9 +124,10 @@ for f in range(FR):
                 fn(exact, f)
             return go
         copy_only = time_ms(lambda: exact.tmp_data.copy_(saved))
-        res["fitter_ms"] = {"valu_exact": time_ms(again(valu_fitter)) - copy_only,
-                            "mfma_compact_wy": time_ms(again(wy_fitter)) - copy_only}
-    for sp in (exact, blocked):
+        res["fitter_ms"] = {"valu_exact": time_ms(again(valu_fitter)) - copy_only}
+        for nb in NBS:
+            res["fitter_ms"][f"mfma_compact_wy_nb{nb}"] = time_ms(again(wy_fitter_nb(nb))) - copy_only
+    for sp in [exact] + list(blocked.values()):
         sp.swap()
 # the production K1 (f32 tmp_data) for context: fit + everything else of the frame
 den = bmfr_amd.Denoiser(cfg)

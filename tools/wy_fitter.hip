@@ -1,15 +1,18 @@
 // wy_fitter.hip -- EXPERIMENT (tools-only build, not in libbmfr): the BMFR
 // fitter stage (bmfr.cl:490-700) with a blocked compact-WY Householder QR
 // whose trailing-panel update runs on MFMA (v_mfma_f32_16x16x4_f32), in
-// f32-tmp_data mode, for the B = 13 canonical feature list.
+// f32-tmp_data mode, for the canonical feature lists B = 13 (FS = 6) and
+// B = 16 (FS = 9, BASELINE config 5's 3rd-order set), panels of NB pivot
+// columns (4, 8, or all of them: one full-width panel).
 //
 // Same inputs / outputs as the stage fitter (bmfr_fitter: tmp_data
-// [block][13][1024] f32 -> weights [block][10][3], mins_maxs [block][6][2]).
+// [block][B][1024] f32 -> weights [block][B-3][3], mins_maxs [block][FS][2]).
 // Scaling and noise are the reference's (exact); the QR reassociates:
-//   per panel of nb <= 4 pivot columns: unblocked Householder steps on the
+//   per panel of nb <= NB pivot columns: unblocked Householder steps on the
 //   panel columns (VALU), T of Q = H_0 ... H_{nb-1} = I - V T V^T, then the
 //   trailing columns X_t <- X_t - V (T^T (V^T X_t)) with V^T X_t (K = 1024
-//   rows) and the rank-nb update V W2 as 16x16x4 f32 MFMAs.
+//   rows) and the rank-nb update V W2 as 16x16x4 f32 MFMAs (ceil(nb / 4)
+//   k-steps of 4).
 // Back substitution as the reference (bmfr.cl:658-699).  Tolerance-checked
 // against the reference (tools/mfma_experiment.py), never bit-exact.
 #include <hip/hip_runtime.h>
@@ -18,19 +21,21 @@
 
 namespace {
 
-constexpr int B = 13, NS = 4, FS = 6, NF = B - 3, RE = B - 2;
+constexpr int NS = 4;
 constexpr int kRows = 1024, kThreads = 256;
-constexpr int kX = B;  // LDS row stride of the block matrix (odd: conflict-free row-per-lane access)
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+template <int B, int FS>
 struct Lds {
+    static constexpr int NF = B - 3, RE = B - 2;
+    static constexpr int kX = B | 1;  // LDS row stride of the block matrix (odd: conflict-free row-per-lane access)
     float X[kRows * kX];       // block matrix, row-major
     float red[4][16];          // cross-wave reduction scratch
-    float Wp[4][4][16];        // per-wave partial V^T X
-    float W2[4][16];           // T^T V^T X
-    float T[4][4];
-    float gram[4][4];
+    float Wp[4][16][16];       // per-wave partial V^T X
+    float W2[16][16];          // T^T V^T X
+    float T[16][16];
+    float gram[16][16];
     float ucl2[NF], ulen2[NF];
     float R[RE * RE * 3];      // R[x][y][ch], x = column
     float weights[NF * 3];
@@ -44,7 +49,8 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // Block-wide sum of one value per thread (any association: tolerance mode).
-__device__ __forceinline__ float block_sum(float v, Lds& L, int t) {
+template <class L_>
+__device__ __forceinline__ float block_sum(float v, L_& L, int t) {
     v = wave_sum(v);
     __syncthreads();
     if ((t & 63) == 0) L.red[t >> 6][0] = v;
@@ -53,13 +59,18 @@ __device__ __forceinline__ float block_sum(float v, Lds& L, int t) {
 }
 
 // V[r][c] of the reflector of pivot column c: zero above the pivot, u_c below.
-__device__ __forceinline__ float vval(const Lds& L, int r, int c) {
-    return r < c ? 0.f : (r == c ? L.ucl2[c] : L.X[r * kX + c]);
+template <class L_>
+__device__ __forceinline__ float vval(const L_& L, int r, int c) {
+    return r < c ? 0.f : (r == c ? L.ucl2[c] : L.X[r * L_::kX + c]);
 }
 
+template <int B, int FS, int NB>
 __global__ __launch_bounds__(kThreads) void k_fitter_wy(const float* __restrict__ tmp, float* __restrict__ weights,
                                                         float* __restrict__ mins_maxs, int frame, double noise2) {
-    __shared__ Lds L;
+    static_assert(B <= 16 && NB <= 16, "16x16 MFMA tiles");
+    using L_ = Lds<B, FS>;
+    constexpr int NF = L_::NF, RE = L_::RE, kX = L_::kX;
+    __shared__ L_ L;
     const int t = threadIdx.x, w = t >> 6, l = t & 63, g = blockIdx.x;
     const float* src = tmp + (size_t)g * B * kRows;
     // ---- load, min/max scaling (bmfr.cl:510-542), noise (bmfr.cl:625-627) ----
@@ -106,8 +117,8 @@ __global__ __launch_bounds__(kThreads) void k_fitter_wy(const float* __restrict_
     __syncthreads();
 
     // ---- blocked Householder QR ----
-    for (int j0 = 0; j0 < NF; j0 += 4) {
-        const int nb = NF - j0 < 4 ? NF - j0 : 4;
+    for (int j0 = 0; j0 < NF; j0 += NB) {
+        const int nb = NF - j0 < NB ? NF - j0 : NB;
         // panel factorization, unblocked (VALU)
         for (int c = j0; c < j0 + nb; ++c) {
             float sq = 0.f;
@@ -158,8 +169,8 @@ __global__ __launch_bounds__(kThreads) void k_fitter_wy(const float* __restrict_
         }
         __syncthreads();
         if (t == 0) {
-            for (int i = 0; i < 4; ++i)
-                for (int k = 0; k < 4; ++k) L.T[i][k] = 0.f;
+            for (int i = 0; i < 16; ++i)
+                for (int k = 0; k < 16; ++k) L.T[i][k] = 0.f;
             for (int i = 0; i < nb; ++i) {
                 const float tau = 2.f / L.ulen2[j0 + i];
                 L.T[i][i] = tau;
@@ -182,11 +193,10 @@ __global__ __launch_bounds__(kThreads) void k_fitter_wy(const float* __restrict_
             const float b = j < B ? L.X[r * kX + j] : 0.f;
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
         }
-        // D[i][j]: lane l holds rows i = 4 (l / 16) + e, column j = l % 16; rows < nb live in lanes 0..15
-        if (l < 16)
-            for (int e = 0; e < 4; ++e) L.Wp[w][e][l] = acc[e];
+        // D[i][j]: lane l holds rows i = 4 (l / 16) + e, column j = l % 16
+        for (int e = 0; e < 4; ++e) L.Wp[w][4 * (l >> 4) + e][l & 15] = acc[e];
         __syncthreads();
-        if (t < 64) {  // W2 = -(T^T W) on the trailing columns, zero elsewhere
+        {  // W2 = -(T^T W) on the trailing columns, zero elsewhere
             const int i = t >> 4, j = t & 15;
             float v = 0.f;
             if (i < nb && j >= jt && j < B)
@@ -195,15 +205,20 @@ __global__ __launch_bounds__(kThreads) void k_fitter_wy(const float* __restrict_
             L.W2[i][j] = -v;
         }
         __syncthreads();
-        // X_t += V (-W2) on MFMA, 16-row tiles: A (16 x 4): lane l -> V[r0 + l % 16][j0 + l / 16];
-        // B (4 x 16): lane l -> -W2[l / 16][l % 16]; C / D: rows r0 + 4 (l / 16) + e, column l % 16.
+        // X_t += V (-W2) on MFMA, 16-row tiles, ceil(nb / 4) k-steps: A (16 x 4): lane l ->
+        // V[r0 + l % 16][j0 + 4 kk + l / 16]; B (4 x 16): lane l -> -W2[4 kk + l / 16][l % 16];
+        // C / D: rows r0 + 4 (l / 16) + e, column l % 16.
+        if (jt < B)
         for (int tile = w; tile < kRows / 16; tile += 4) {
             const int r0 = 16 * tile, j = l & 15, q = l >> 4;
-            const float a = q < nb ? vval(L, r0 + j, j0 + q) : 0.f;
-            const float b = L.W2[q][j];
-            f4 c;
-            for (int e = 0; e < 4; ++e) c[e] = j < B ? L.X[(r0 + 4 * q + e) * kX + j] : 0.f;
-            const f4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+            f4 d;
+            for (int e = 0; e < 4; ++e) d[e] = j < B ? L.X[(r0 + 4 * q + e) * kX + j] : 0.f;
+            for (int kk = 0; 4 * kk < nb; ++kk) {
+                const int vc = 4 * kk + q;
+                const float a = vc < nb ? vval(L, r0 + j, j0 + vc) : 0.f;
+                const float b = L.W2[vc][j];
+                d = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, d, 0, 0, 0);
+            }
             // (V reads the panel columns, the writes go to trailing columns of this wave's rows)
             if (j >= jt && j < B)
                 for (int e = 0; e < 4; ++e) L.X[(r0 + 4 * q + e) * kX + j] = d[e];
@@ -243,9 +258,15 @@ __global__ __launch_bounds__(kThreads) void k_fitter_wy(const float* __restrict_
 
 }  // namespace
 
+// buffers = B (13 or 16), nb = panel width (4, 8 or 16: the whole QR in one panel).
 extern "C" int wy_fitter(int blocks, const float* tmp, float* weights, float* mins_maxs, int frame, double noise2,
-                         void* stream) {
-    hipLaunchKernelGGL(k_fitter_wy, dim3(blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream), tmp, weights,
-                       mins_maxs, frame, noise2);
+                         void* stream, int buffers, int nb) {
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+#define WY(B_, FS_, NB_)                                                                                 \
+    if (buffers == B_ && nb == NB_)                                                                      \
+        hipLaunchKernelGGL((k_fitter_wy<B_, FS_, NB_>), dim3(blocks), dim3(kThreads), 0, st, tmp, weights, \
+                           mins_maxs, frame, noise2);
+    WY(13, 6, 4) WY(13, 6, 8) WY(13, 6, 16) WY(16, 9, 4) WY(16, 9, 8) WY(16, 9, 16)
+#undef WY
     return (int)hipGetLastError();
 }
