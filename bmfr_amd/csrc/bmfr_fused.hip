@@ -473,11 +473,11 @@ template <int NS, int FS, class IN>
 __global__ __launch_bounds__(kThreads) void k_fused_rows_taa(Params P, K1Args A, TaaArgs T, int nk1, int nk1p) {
     __shared__ union {
         K1Lds<NS + FS + 3> k1;
-        FrameTaaLds k2;
+        FrameTaaLds<kThreads> k2;
     } U;
     const int b = blockIdx.x;
     if (b < nk1) k1_rows_body<NS, FS, IN, true>(P, A, U.k1, xcd_swizzle(b, nk1));
-    else if (b >= nk1p) frame_taa_part<IN, true>(P, T, b, nk1p, U.k2);
+    else if (b >= nk1p) frame_taa_part<IN, true, kThreads>(P, T, b, nk1p, U.k2);
 }
 
 bool fused_supported(const Params& P) {
@@ -495,8 +495,8 @@ static void launch_k1(const Params& P, hipStream_t st, const FusedArgs& A) {
 template <int FS, class IN>
 static void launch_rows_frame(const Params& P, hipStream_t st, const FusedArgs& A) {
     const int nk1 = P.ring < 0 || P.nbx <= 0 || P.nby <= 0 ? 0 : k1_blocks(P), nk1p = (nk1 + 7) & ~7;
-    hipLaunchKernelGGL((k_fused_rows_taa<4, FS, IN>), dim3(nk1p + frame_taa_tiles(P)), dim3(kThreads), 0, st, P,
-                       k1_args(A), taa_args(A), nk1, nk1p);
+    hipLaunchKernelGGL((k_fused_rows_taa<4, FS, IN>), dim3(nk1p + frame_taa_tiles<kThreads>(P)), dim3(kThreads), 0,
+                       st, P, k1_args(A), taa_args(A), nk1, nk1p);
 }
 
 hipError_t launch_fused_rows_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {

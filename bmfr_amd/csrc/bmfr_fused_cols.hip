@@ -34,7 +34,13 @@
 namespace bmfr {
 namespace cols {
 
-constexpr int kThreads = 256;
+// Waves per work-group NW = 4 (the default) or 8: 64 NW threads; in phase 1
+// and 3 a thread owns kItems = 16 / NW rows of the block.
+constexpr int kThreads = 256;  // NW = 4
+template <int NW>
+constexpr int threads_of() { return 64 * NW; }
+template <int NW>
+constexpr int items_of() { return 16 / NW; }
 constexpr int kSlots = 16;    // rows per lane per column (row = lane + 64 j)
 constexpr int kUStride = 20;     // floats per lane in a u buffer: 16 + 4 (conflict-free 16-byte reads)
 constexpr int kPre = 2;          // step-0 noise columns per wave prefetched in phase 1
@@ -48,11 +54,11 @@ constexpr int kUBufs = 3;
 // buffers (B >= 16) they wait in registers until the fit has loaded its
 // columns and then go there, so the work-group's LDS stays within 40 KB (four
 // work-groups per CU); otherwise they have their own LDS array.
-constexpr int kKeep = 4 * 3 * kThreads;
+constexpr int kKeep = 16 * 3 * 64;  // 12 floats per thread at NW = 4, 6 at NW = 8
 constexpr bool keep_in_m(int B) {
     return (B - 1) * 64 * kSlots * 2 >= (kUBufs * 64 * kUStride + kKeep) * 4;
 }
-template <int B>
+template <int B, int NW = 4>
 struct Lds {
     union {
         _Float16 M[B - 1][64 * kSlots];  // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
@@ -62,10 +68,10 @@ struct Lds {
         };
     };
     float keep_s[keep_in_m(B) ? 1 : kKeep];
-    __device__ float* keep() { return keep_in_m(B) ? keep_m : keep_s; }  // [(item * 3 + ch) * kThreads + t]
+    __device__ float* keep() { return keep_in_m(B) ? keep_m : keep_s; }  // [(item * 3 + ch) * 64 NW + t]
     float piv[kUBufs][2];               // |u|^2 and RN(1/|u|^2) of the published vector
     int pub;                            // highest published pivot column
-    int prog[4];                        // per wave: the last step it has applied
+    int prog[NW];                       // per wave: the last step it has applied
     int timeout;                        // a flag wait of this block gave up (reported once, at the end)
     int max_polls;                      // Params::max_polls (kept here: read only once a flag is not ready)
     int delay;                          // Params::debug_delay (diagnostics, read at the block's end)
@@ -244,8 +250,8 @@ __device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const float* _
 // marks the block (*timeout), the block reports BMFR_ERROR_SYNC_TIMEOUT
 // (report_sync_timeout) and runs to its end -- a scheduling bug gives a
 // reported error, never a wave that never finishes nor silently wrong pixels.
-template <int B>
-__device__ __forceinline__ void wait_flag(Lds<B>& L, const int* flag, int c) {
+template <class LDS>
+__device__ __forceinline__ void wait_flag(LDS& L, const int* flag, int c) {
     if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= c) return;
     const int mp = L.max_polls;
     for (int k = 0;; ++k) {
@@ -257,20 +263,20 @@ __device__ __forceinline__ void wait_flag(Lds<B>& L, const int* flag, int c) {
         if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= c) return;
     }
 }
-template <int B>
-__device__ __forceinline__ void wait_pub(Lds<B>& L, int c) {
+template <int B, int NW>
+__device__ __forceinline__ void wait_pub(Lds<B, NW>& L, int c) {
     wait_flag(L, &L.pub, c);
 }
-template <int B>
-__device__ __forceinline__ void wait_all_progress(Lds<B>& L, int c) {
-    for (int w = 0; w < 4; ++w) wait_flag(L, &L.prog[w], c);
+template <int B, int NW>
+__device__ __forceinline__ void wait_all_progress(Lds<B, NW>& L, int c) {
+    for (int w = 0; w < NW; ++w) wait_flag(L, &L.prog[w], c);
 }
 
 // The owner of pivot column c (>= 1), once steps 0..c-1 are applied to it:
 // |x|^2 over rows >= c+1, the Householder vector u and |u|^2 (bmfr.cl:555-601),
 // published to LDS with the R column.
-template <int c, int B>
-__device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B>& L, int l) {
+template <int c, int B, int NW>
+__device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B, NW>& L, int l) {
     constexpr int RE = B - 2;
     float x[kSlots];
 #pragma unroll
@@ -320,28 +326,31 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B>& L, int l
 // wait for its global loads and stores (__syncthreads() does).
 __device__ __forceinline__ void k1_barrier() { lds_barrier(); }
 
-// Wave W's part of the fit: columns c = 1 + W + 4 k (slot k); column 0 is
-// implicit.  W is a run-time (wave-uniform) value, so the four waves run one
+// Wave W's part of the fit: columns c = 1 + W + NW k (slot k); column 0 is
+// implicit.  W is a run-time (wave-uniform) value, so the NW waves run one
 // copy of the code: column ownership is a scalar branch, while the slot of
 // every column a step touches is known at compile time.
-template <int NS, int FS>
+template <int NS, int FS, int NW = 4>
 struct WaveFit {
     static constexpr int B = NS + FS + 3;
     static constexpr int NF = B - 3;  // pivot columns
-    static constexpr int NSL = (B + 2) / 4;
-    static __device__ __forceinline__ bool owns(int W, int c) { return c >= 1 && c < B && ((c - 1) & 3) == W; }
-    static constexpr int owner(int c) { return (c - 1) & 3; }
-    static constexpr int slot(int c) { return (c - 1) >> 2; }
-    // Step-0 noise columns prefetched per wave: none at B = 16, where the
-    // fit's registers are the limit for four work-groups per CU.
-    static constexpr int NP = B >= 16 ? 0 : kPre;
+    static constexpr int NSL = (B - 1 + NW - 1) / NW;
+    static constexpr int NT = 64 * NW, NI = 16 / NW;  // threads, items (rows) per thread in phases 1 and 3
+    using LDS = Lds<B, NW>;
+    static __device__ __forceinline__ bool owns(int W, int c) { return c >= 1 && c < B && (c - 1) % NW == W; }
+    static constexpr int owner(int c) { return (c - 1) % NW; }
+    static constexpr int slot(int c) { return (c - 1) / NW; }
+    // Step-0 noise columns prefetched per wave (slots whose column is a
+    // feature column for every wave): none at B = 16 with four waves, where
+    // the fit's registers are the limit for four work-groups per CU.
+    static constexpr int NP = B >= 16 && NW == 4 ? 0 : ((NF - 1) / NW < kPre ? (NF - 1) / NW : kPre);
+    static_assert(NP == 0 || NW * NP < NF, "prefetched slots hold feature columns");
 
     // The first column a wave updates at step 0: a feature column for every wave.
     static __device__ __forceinline__ int first_column(int W) { return 1 + W; }
-    static_assert(5 + 3 < NF, "the first two columns of every wave are feature columns");
 
     template <int c>
-    static __device__ __forceinline__ void step(h2 (&a)[NSL][8], Lds<B>& L, int W, int l,
+    static __device__ __forceinline__ void step(h2 (&a)[NSL][8], LDS& L, int W, int l,
                                                 const float* __restrict__ noise, const float (&pre)[kPre][kSlots],
                                                 double noise2) {
         constexpr int nxt = c + 1;  // the next pivot column, slot(nxt) of wave owner(nxt)
@@ -353,13 +362,13 @@ struct WaveFit {
             }
             sfor<NSL>([&](auto K) {
                 constexpr int k = decltype(K)::value;
-                const int fb = 1 + W + 4 * k;
+                const int fb = 1 + W + NW * k;
                 if (owns(W, fb) && !(publish && fb == nxt))  // slots < NP: feature columns, prefetched
                     update_column0(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr,
                                    pre[k < kPre ? k : 0], k < NP, noise2);
             });
         } else {
-            if (1 + W + 4 * ((B - 2 - W) / 4) > c) {  // this wave's last column is past the pivot
+            if (1 + W + NW * ((B - 2 - W) / NW) > c) {  // this wave's last column is past the pivot
                 wait_pub(L, c);
                 float u[kSlots];
                 const float4* src = reinterpret_cast<const float4*>(&L.u[c % kUBufs][l * kUStride]);
@@ -380,8 +389,8 @@ struct WaveFit {
                 }
                 sfor<NSL>([&](auto K) {
                     constexpr int k = decltype(K)::value;
-                    const int fb = 1 + W + 4 * k;
-                    if constexpr (4 * k + 4 > c) {  // slot k holds columns <= 4k + 4
+                    const int fb = 1 + W + NW * k;
+                    if constexpr (NW * k + NW > c) {  // slot k holds columns <= NW k + NW
                         if (owns(W, fb) && fb > c && !(publish && fb == nxt))
                             update_column<c>(a[k], u, ulen2, recip, l);
                     }
@@ -393,33 +402,33 @@ struct WaveFit {
     }
 
     template <int... C>
-    static __device__ __forceinline__ void steps(h2 (&a)[NSL][8], Lds<B>& L, int W, int l,
+    static __device__ __forceinline__ void steps(h2 (&a)[NSL][8], LDS& L, int W, int l,
                                                  const float* __restrict__ noise, const float (&pre)[kPre][kSlots],
                                                  double noise2, std::integer_sequence<int, C...>) {
         (step<C>(a, L, W, l, noise, pre, noise2), ...);
     }
 
-    // Step 0's noise for the wave's first kPre columns (1 + W, 5 + W: feature
-    // columns for every wave), loaded while the last items of phase 1 finish
-    // (the fit's first dependent loads); with B = 13 only wave 0 has a third
-    // noisy column, loaded in step 0.
+    // Step 0's noise for the wave's first NP columns (1 + W, 1 + W + NW:
+    // feature columns for every wave), loaded while the last items of phase 1
+    // finish (the fit's first dependent loads); the other noisy columns load
+    // in step 0.
     static __device__ __forceinline__ void prefetch_noise(int W, int l, const float* __restrict__ noise,
                                                           float (&pre)[kPre][kSlots]) {
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
-            const float* src = noise + (first_column(W) + 4 * k - 1) * kBlockPixels + l;
+            const float* src = noise + (first_column(W) + NW * k - 1) * kBlockPixels + l;
 #pragma unroll
             for (int j = 0; j < kSlots; ++j) pre[k][j] = src[64 * j];
         }
     }
 
-    static __device__ __forceinline__ void run(Lds<B>& L, int W, int l, const float* __restrict__ noise,
+    static __device__ __forceinline__ void run(LDS& L, int W, int l, const float* __restrict__ noise,
                                                const float (&pre)[kPre][kSlots], double noise2, int mp,
-                                               const float (&kp)[4][3]) {
+                                               const float (&kp)[NI][3]) {
         h2 a[NSL][8];
         sfor<NSL>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            const int c = 1 + W + 4 * k;
+            const int c = 1 + W + NW * k;
             if (owns(W, c)) {
                 // pair p of lane l's row slot sits at dword p ^ ((l >> 2) & 7) (see phase 1)
                 const uint32_t* src = reinterpret_cast<const uint32_t*>(&L.M[c - 1][l * kSlots]);
@@ -428,25 +437,25 @@ struct WaveFit {
                 for (int i = 0; i < 8; ++i) a[k][i] = __builtin_bit_cast(h2, src[i ^ q]);
             }
         });
-        if (W == 0 && l < 7) {  // read only after the barrier below
+        if (W == 0 && l < NW + 3) {  // read only after the barrier below
             if (l == 0) L.pub = 0;
-            else if (l == 5) L.timeout = 0;
-            else if (l == 6) L.max_polls = mp;
+            else if (l == NW + 1) L.timeout = 0;
+            else if (l == NW + 2) L.max_polls = mp;
             else L.prog[l - 1] = -1;
         }
         k1_barrier();  // the u buffers alias M
         if constexpr (keep_in_m(B)) {  // phase 1's kept colours into the matrix area beside the u buffers
             const int t = W * 64 + l;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < NI; ++i)
 #pragma unroll
-                for (int ch = 0; ch < 3; ++ch) L.keep_m[(i * 3 + ch) * kThreads + t] = kp[i][ch];
+                for (int ch = 0; ch < 3; ++ch) L.keep_m[(i * 3 + ch) * NT + t] = kp[i][ch];
         }
 
         // Scale the position features to the block's [min, max] (bmfr.cl:510-542).
         sfor<NSL>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            const int c = 1 + W + 4 * k;
+            const int c = 1 + W + NW * k;
             if (owns(W, c) && c >= NS && c < NF) {
                 float hi[4], lo[4];
 #pragma unroll
@@ -484,7 +493,7 @@ struct WaveFit {
         // Right-hand side: rows 0..B-4 of the colour columns (bmfr.cl:596-600).
         sfor<NSL>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            const int c = 1 + W + 4 * k;
+            const int c = 1 + W + NW * k;
             if (owns(W, c) && c >= NF) {
                 if (l < NF) L.R[((B - 3) * (B - 2) + l) * 3 + (c - NF)] = hget(a[k], 0);
             }
@@ -510,8 +519,8 @@ template <int N>
 __device__ __forceinline__ float row_bcast(float v) {  // every lane <- lane N of its row
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + N, 0xf, 0xf, false));
 }
-template <int B>
-__device__ __forceinline__ void back_substitute_regs(Lds<B>& L, int t) {
+template <int B, int NW>
+__device__ __forceinline__ void back_substitute_regs(Lds<B, NW>& L, int t) {
     constexpr int RE = B - 2;
     static_assert(RE <= 16, "one DPP row per channel");
     if (t >= 64) return;
@@ -556,9 +565,10 @@ constexpr int kColsWaves = 4;  // minimum waves per SIMD for the register alloca
 // COH: the TAA tiles of the same frame run in this launch: the accumulated
 // colour and the reprojected positions they read are stored device-coherent
 // and the block publishes done[g] = epoch once they are.
-template <int NS, int FS, class IN, bool COH = false>
-__device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, Lds<NS + FS + 3>& L, int g) {
+template <int NS, int FS, class IN, bool COH = false, int NW = 4>
+__device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, Lds<NS + FS + 3, NW>& L, int g) {
     constexpr int B = NS + FS + 3;
+    constexpr int NT = 64 * NW, NI = 16 / NW;  // threads; items (rows) per thread
     const int t = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int l = t & 63;
@@ -580,9 +590,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // LDS until the end (fewer scalar registers live across the kernel)
     if constexpr (COH)
         if (t == 0) L.flag = (by - P.by0) * P.nbx + (bx - P.bx0);
-    const int lx = l & (kEdge - 1), ly = (l >> 5) + 8 * w;  // item i: row y = ly + 2 i
+    const int lx = l & (kEdge - 1), ly = (l >> 5) + 2 * NI * w;  // item i: row y = ly + 2 i
 
-    // ---- accumulate_noisy_data (bmfr.cl:310-484), rows l + 64 (4w + i) ----
+    // ---- accumulate_noisy_data (bmfr.cl:310-484), rows l + 64 (NI w + i) ----
     h2 pk[B];            // features of an item pair, packed for one 4-byte LDS store per column
     uint32_t spps = 0;   // per item i, bits 8i..8i+7: its new spp
     uint32_t ibits = 0;  // per item i, bit i: owner; bit 4 + i: accepted taps with weight > 0
@@ -592,13 +602,13 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // Software-pipelined one item deep: item i + 1's current-frame loads go
     // out right behind item i's reprojection taps, so each wait for taps
     // leaves the next item's loads in flight.
-    float kp[4][3];  // keep_in_m(B): the kept colours, in registers until the fit has loaded M
+    float kp[NI][3];  // keep_in_m(B): the kept colours, in registers until the fit has loaded M
     NoisyCur<IN> cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly, frame);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
         const NoisyTaps<IN> tp = noisy_taps_issue<true, IN>(P, A.in, A.cam, cur, frame, A.acc_prev);
         NoisyCur<IN> nxt;
-        if (i < 3) nxt = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly + 2 * (i + 1), frame);
+        if (i < NI - 1) nxt = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly + 2 * (i + 1), frame);
         __builtin_amdgcn_sched_barrier(0);
         const NoisyItem it = noisy_taps_finish<true, IN>(P, cur, tp, frame);
         {
@@ -620,9 +630,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 kp[i][1] = it.prev_f.y;
                 kp[i][2] = it.prev_f.z;
             } else {
-                L.keep_s[(i * 3 + 0) * kThreads + t] = it.prev_f.x;
-                L.keep_s[(i * 3 + 1) * kThreads + t] = it.prev_f.y;
-                L.keep_s[(i * 3 + 2) * kThreads + t] = it.prev_f.z;
+                L.keep_s[(i * 3 + 0) * NT + t] = it.prev_f.x;
+                L.keep_s[(i * 3 + 1) * NT + t] = it.prev_f.y;
+                L.keep_s[(i * 3 + 2) * NT + t] = it.prev_f.z;
             }
             if (it.owner) {
                 st3(A.noisy_out, it.lin, it.color);
@@ -630,37 +640,37 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 if constexpr (COH) st2_coh(coh_plane(A.prev_pixel_out), it.lin, make_float2(it.pfx, it.pfy));
                 else st_px(A.prev_pixel_out, it.lin, make_float2(it.pfx, it.pfy));
             }
-            if (i & 1) {  // rows j = 4w + i - 1, 4w + i: adjacent halves of lane l's row slot
-                // (pair 2w + i/2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)
-                const int pair = (2 * w + i / 2) ^ ((l >> 2) & 7);
+            if (i & 1) {  // rows j = NI w + i - 1, NI w + i: adjacent halves of lane l's row slot
+                // (pair (NI w + i) / 2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)
+                const int pair = ((NI * w + i) / 2) ^ ((l >> 2) & 7);
 #pragma unroll
                 for (int f = 1; f < B; ++f)
                     *reinterpret_cast<uint32_t*>(&L.M[f - 1][l * kSlots + 2 * pair]) = __builtin_bit_cast(uint32_t, pk[f]);
             }
         }
-        if (i < 3) cur = nxt;
+        if (i < NI - 1) cur = nxt;
     }
     report_reach(P, A.reach, over);
     float pre[kPre][kSlots];
-    WaveFit<NS, FS>::prefetch_noise(w, l, A.noise, pre);
+    WaveFit<NS, FS, NW>::prefetch_noise(w, l, A.noise, pre);
     k1_barrier();  // matrix in LDS; phase 1's global stores drain in the background
     BMFR_STAMP(1);
     BMFR_STAMP(2);  // scaling runs inside the per-wave fit
 
     // ---- fit: min/max scaling, Householder QR, right-hand side ----
     if (t == 0) L.delay = P.debug_delay;  // read after the fit's barriers
-    WaveFit<NS, FS>::run(L, w, l, A.noise, pre, P.noise2, P.max_polls, kp);
-    // Phase 3's loads (normal and position of the four items, bmfr.cl:725-729)
+    WaveFit<NS, FS, NW>::run(L, w, l, A.noise, pre, P.noise2, P.max_polls, kp);
+    // Phase 3's loads (normal and position of the NI items, bmfr.cl:725-729)
     // go out now: they land while wave 0 back-substitutes and the others wait.
     int l3 = l;  // opaque copy: recompute phase-1 addresses instead of keeping them live across the fit
     asm volatile("" : "+v"(l3));
     const int2 off = kBlockOffsets[frame & 15];
-    uint32_t lin[4];
-    In3<IN> nrm_r[4], wp_r[4];  // as loaded: widened after the back substitution
+    uint32_t lin[NI];
+    In3<IN> nrm_r[NI], wp_r[NI];  // as loaded: widened after the back substitution
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
         const int px = bx * kEdge + (l3 & (kEdge - 1)) - kEdge / 2 + off.x;
-        const int py = by * kEdge + (l3 >> 5) + 8 * w + 2 * i - kEdge / 2 + off.y;
+        const int py = by * kEdge + (l3 >> 5) + 2 * NI * w + 2 * i - kEdge / 2 + off.y;
         lin[i] = pix(P, (ibits & (1u << i)) ? px : P.ox, (ibits & (1u << i)) ? py : P.oy);  // margins: a valid pixel, skipped below
         nrm_r[i] = ld3raw<IN>(A.in.n_cur, lin[i]);
         wp_r[i] = ld3raw<IN>(A.in.p_cur, lin[i]);
@@ -675,9 +685,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     if constexpr (!COH)
         if (t == 0 && L.timeout) report_sync_timeout(A.sync_err, kSyncPivot, frame);
     BMFR_STAMP(4);
-    f3 nrm[4], wp[4];
+    f3 nrm[NI], wp[NI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
         nrm[i] = widen(nrm_r[i]);
         wp[i] = widen(wp_r[i]);
     }
@@ -685,9 +695,10 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // ---- weighted_sum (bmfr.cl:717-750) + temporal blend (bmfr.cl:778-849) ----
     // Items (0, 1) and (2, 3) as packed f32 pairs: every lane rounds as
     // upstream's scalar sequence, each item in feature order.
-    f2v cp[2][3];
+    constexpr int NPR = NI / 2;  // item pairs
+    f2v cp[NPR][3];
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < NPR; ++h)
         for (int ch = 0; ch < 3; ++ch) cp[h][ch] = f2v{0.f, 0.f};
     // Item pairs outer where it saves registers: one pair's positions, powers
     // and sums live at a time (features outer kept every item's in registers:
@@ -698,9 +709,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 #ifdef PAIRS_ALL
     constexpr bool kPairs = true;
 #else
-    constexpr bool kPairs = B >= 16 || !COH;
+    constexpr bool kPairs = B >= 16 || !COH || NPR == 1;
 #endif
-    constexpr int NH = kPairs ? 2 : 1;
+    constexpr int NH = kPairs ? NPR : 1;
 #pragma unroll
     for (int hh = 0; hh < NH; ++hh) {
 #pragma unroll
@@ -715,7 +726,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 rcp = L.mm[3 * (f - NS) + 2];
             }
 #pragma unroll
-            for (int h = kPairs ? hh : 0; h < (kPairs ? hh + 1 : 2); ++h) {
+            for (int h = kPairs ? hh : 0; h < (kPairs ? hh + 1 : NPR); ++h) {
                 f2v v = {feature_value(f, nrm[2 * h], wp[2 * h]), feature_value(f, nrm[2 * h + 1], wp[2 * h + 1])};
                 if (f >= NS) {
                     v = v - f2v{bmin, bmin};
@@ -732,7 +743,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
         }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
         if (ibits & (1u << i)) {
             f3 ci{cp[i >> 1][0][i & 1], cp[i >> 1][1][i & 1], cp[i >> 1][2][i & 1]};
             ci.x = ci.x < 0.f ? 0.f : ci.x;
@@ -745,7 +756,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
             const float beta = 1.f - alpha;
             const int t3 = l3 + 64 * w;
             const float* kb = L.keep();
-            const f3 prev{kb[(i * 3) * kThreads + t3], kb[(i * 3 + 1) * kThreads + t3], kb[(i * 3 + 2) * kThreads + t3]};
+            const f3 prev{kb[(i * 3) * NT + t3], kb[(i * 3 + 1) * NT + t3], kb[(i * 3 + 2) * NT + t3]};
             const f3 acc{alpha * ci.x + beta * prev.x, alpha * ci.y + beta * prev.y, alpha * ci.z + beta * prev.z};
             if constexpr (COH) st3_coh(coh_plane(A.acc_out), lin[i], acc);
             else st3(A.acc_out, lin[i], acc);
@@ -771,10 +782,26 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     }
 }
 
+// Waves per work-group of the column-split K1: 4, or 8 with -DBMFR_K1_WAVES=8
+// (half the rows per thread in phases 1 and 3, fewer columns per wave in the
+// fit, more waves per CU).
+#ifndef BMFR_K1_WAVES
+#define BMFR_K1_WAVES 4
+#endif
+constexpr int kNW = BMFR_K1_WAVES;
+constexpr int kK1Threads = 64 * kNW;
+// Minimum waves per SIMD for the register allocator: 4 work-groups of 4
+// waves per CU (128 VGPRs), or 3 of 8 (80); -DBMFR_K1_MIN_WAVES overrides.
+#ifdef BMFR_K1_MIN_WAVES
+constexpr int kMinWavesSimd = BMFR_K1_MIN_WAVES;
+#else
+constexpr int kMinWavesSimd = kNW == 4 ? 4 : 6;
+#endif
+
 template <int NS, int FS, class IN>
-__global__ __launch_bounds__(kThreads, kColsWaves) void k_fused_cols(Params P, K1Args A) {
-    __shared__ Lds<NS + FS + 3> L;
-    k1_cols_body<NS, FS, IN>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
+__global__ __launch_bounds__(kK1Threads, kMinWavesSimd) void k_fused_cols(Params P, K1Args A) {
+    __shared__ Lds<NS + FS + 3, kNW> L;
+    k1_cols_body<NS, FS, IN, false, kNW>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
 }
 
 // K1 and K2 (64 x kFrameTaaH tiles) in one launch: work-groups [0, nk1) are K1
@@ -791,15 +818,15 @@ __global__ __launch_bounds__(kThreads, kColsWaves) void k_fused_cols(Params P, K
 //     in order, so every K1 block a waiting tile needs has been dispatched:
 //     the waits end.
 template <int NS, int FS, class IN, bool SAME = false>
-__global__ __launch_bounds__(kThreads, 4) void k_fused_cols_taa(Params P, K1Args A, Params P2, TaaArgs T, int nk1,
-                                                                int nk1p) {
+__global__ __launch_bounds__(kK1Threads, kMinWavesSimd) void k_fused_cols_taa(Params P, K1Args A, Params P2,
+                                                                              TaaArgs T, int nk1, int nk1p) {
     __shared__ union {
-        Lds<NS + FS + 3> k1;
-        FrameTaaLds k2;
+        Lds<NS + FS + 3, kNW> k1;
+        FrameTaaLds<kK1Threads> k2;
     } U;
     const int b = blockIdx.x;
-    if (b < nk1) k1_cols_body<NS, FS, IN, SAME>(P, A, U.k1, xcd_swizzle(b, nk1));
-    else if (b >= nk1p) frame_taa_part<IN, SAME>(P2, T, b, nk1p, U.k2);
+    if (b < nk1) k1_cols_body<NS, FS, IN, SAME, kNW>(P, A, U.k1, xcd_swizzle(b, nk1));
+    else if (b >= nk1p) frame_taa_part<IN, SAME, kK1Threads>(P2, T, b, nk1p, U.k2);
 }
 
 }  // namespace cols
@@ -808,7 +835,7 @@ bool fused_cols_supported(const Params& P) { return P.half_tmp && fused_supporte
 
 template <int FS, class IN>
 static void launch_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
-    hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN>), dim3(k1_blocks(P)), dim3(cols::kThreads), 0, st, P,
+    hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN>), dim3(k1_blocks(P)), dim3(cols::kK1Threads), 0, st, P,
                        k1_args(A));
 }
 
@@ -821,9 +848,9 @@ bool frame_fused_supported(const Params& P) { return fused_supported(P); }
 template <int FS, class IN>
 static void launch_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
     const int nk1 = P.ring < 0 || P.nbx <= 0 || P.nby <= 0 ? 0 : k1_blocks(P), nk1p = (nk1 + 7) & ~7;
-    const int nk2 = frame_taa_tiles(P);
-    hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN, true>), dim3(nk1p + nk2), dim3(cols::kThreads), 0, st, P,
-                       k1_args(A), P, taa_args(A), nk1, nk1p);
+    const int nk2 = frame_taa_tiles<cols::kK1Threads>(P);
+    hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN, true>), dim3(nk1p + nk2), dim3(cols::kK1Threads), 0, st,
+                       P, k1_args(A), P, taa_args(A), nk1, nk1p);
 }
 
 hipError_t launch_fused_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
@@ -837,10 +864,10 @@ template <int FS, class IN>
 static void launch_cols_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
                             const FusedArgs* A2) {
     const int nk1 = A ? k1_blocks(P) : 0, nk1p = (nk1 + 7) & ~7;
-    const int nk2 = A2 ? frame_taa_tiles(P2) : 0;
+    const int nk2 = A2 ? frame_taa_tiles<cols::kK1Threads>(P2) : 0;
     if (nk1 + nk2 == 0) return;
     const TaaArgs T = A2 ? taa_args(*A2) : TaaArgs{};
-    hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN>), dim3(nk2 ? nk1p + nk2 : nk1), dim3(cols::kThreads), 0,
+    hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN>), dim3(nk2 ? nk1p + nk2 : nk1), dim3(cols::kK1Threads), 0,
                        st, A ? P : P2, k1_args(A ? *A : *A2), A2 ? P2 : P, T, nk1, nk1p);
 }
 

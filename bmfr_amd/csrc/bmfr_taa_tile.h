@@ -136,16 +136,18 @@ __device__ __forceinline__ void forward_reach(const TaaArgs& T, bool here = true
 // Y: (64 + 2) * (TH + 2) float4; sE / sRP: the powr tables' LDS copies.
 // COH: the tile runs in the launch that computes its K1 blocks: it waits for
 // them and reads their outputs with device-coherent loads.
-template <class IN, int TH, bool COH = false>
+// NT threads (NT / 64 rows of 64 per pass).
+template <class IN, int TH, bool COH = false, int NT = 256>
 __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int x0, int y0, float4* __restrict__ Y,
                                          double* __restrict__ sE, double2* __restrict__ sRP) {
-    static_assert(TH % 4 == 0 && TH >= 4, "tile height");
+    constexpr int RP = NT / 64;  // tile rows per pass
+    static_assert(TH % RP == 0 && TH >= RP, "tile height");
     constexpr int HW = 64 + 2, HH = TH + 2, N = HW * HH;
     constexpr int RING = N - 64 * TH;  // halo pixels
-    constexpr int KN = TH / 4;         // output pixels per thread
-    static_assert(RING <= 256, "one ring pixel per thread");
+    constexpr int KN = TH / RP;        // output pixels per thread
+    static_assert(RING <= NT, "one ring pixel per thread");
     const int t = threadIdx.x;
-    bmfr_powr_tables_to_lds<256>(sE, sRP, t);
+    bmfr_powr_tables_to_lds<NT>(sE, sRP, t);
     const int tx = t & (64 - 1), ty = t >> 6;
     if constexpr (COH) wait_k1_blocks(P, T, x0, y0, TH);
     const CohPlane c_pp = coh_plane(T.prev_pixel), c_src = coh_plane(T.src);  // (unused unless COH)
@@ -153,7 +155,7 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
     float2 pf[KN];
 #pragma unroll
     for (int k = 0; k < KN; ++k) {
-        const uint32_t i = pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + ty + 4 * k, P.ty1 - 1));
+        const uint32_t i = pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + ty + RP * k, P.ty1 - 1));
         if constexpr (COH) pf[k] = ld2_coh(c_pp, i);
         else pf[k] = ld_px(T.prev_pixel, i);
     }
@@ -169,7 +171,7 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
     }
 #pragma unroll
     for (int k = 0; k <= KN; ++k) {
-        const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + 4 * k + 1 : hy;
+        const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + RP * k + 1 : hy;
         if (k == KN && t >= RING) break;
         // Clamped into the buffer region (= the image when untiled): a tile
         // whose last 64-px column or TH-row band overhangs its output reads
@@ -187,7 +189,7 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
 #pragma unroll
     for (int k = 0; k <= KN; ++k) {
         if (k == KN && t >= RING) break;
-        const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + 4 * k + 1 : hy;
+        const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + RP * k + 1 : hy;
         v[k] = tone_map(P, widen(al[k]), v[k], sE, sRP);
         const f3 yc = rgb_to_ycocg(v[k]);
         Y[ly * HW + lx] = make_float4(yc.x, yc.y, yc.z, 0.f);
@@ -198,9 +200,9 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
     const bool edge = x0 == 0 || y0 == 0 || x0 + 64 >= P.width || y0 + TH >= P.height;
 #pragma unroll
     for (int k = 0; k < KN; ++k) {
-        const int x = x0 + tx, y = y0 + ty + 4 * k;
+        const int x = x0 + tx, y = y0 + ty + RP * k;
         if (x < P.tx1 && y < P.ty1) {
-            const int c = (ty + 4 * k + 1) * HW + tx + 1;
+            const int c = (ty + RP * k + 1) * HW + tx + 1;
             f3 nb[9];
 #pragma unroll
             for (int j = 0; j < 9; ++j) {
@@ -216,21 +218,26 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
 
 // The TAA part of a one-launch frame kernel (K1 blocks, then the frame's
 // TAA tiles; bmfr_fused_cols.hip k_fused_cols_taa, bmfr_fused.hip
-// k_fused_rows_taa): work-group b >= nk1p of the launch is tile b - nk1p
-// (64 x TH, XCD-aware order).  COH: the tiles wait for the K1 blocks of the
-// same launch; a tiled context's last work-group then forwards the reach
-// report once every K1 block of the launch has raised it.
-constexpr int kFrameTaaH = 12;
+// k_fused_rows_taa) of NT threads per work-group: work-group b >= nk1p of
+// the launch is tile b - nk1p (64 x frame_taa_h<NT>, XCD-aware order).
+// COH: the tiles wait for the K1 blocks of the same launch; a tiled
+// context's last work-group then forwards the reach report once every K1
+// block of the launch has raised it.
+template <int NT>
+constexpr int frame_taa_h() { return NT == 256 ? 12 : 24; }  // 3 output rows per thread
+template <int NT>
 struct FrameTaaLds {
-    float4 Y[(64 + 2) * (kFrameTaaH + 2)];
+    float4 Y[(64 + 2) * (frame_taa_h<NT>() + 2)];
     double sE[kPowrENum];
     double2 sRP[kPowrRPNum];
 };
-template <class IN, bool COH>
-__device__ __forceinline__ void frame_taa_part(const Params& P2, const TaaArgs& T, int b, int nk1p, FrameTaaLds& L) {
+template <class IN, bool COH, int NT>
+__device__ __forceinline__ void frame_taa_part(const Params& P2, const TaaArgs& T, int b, int nk1p,
+                                               FrameTaaLds<NT>& L) {
+    constexpr int TH = frame_taa_h<NT>();
     const int gx = (P2.tx1 - P2.tx0 + 63) / 64, n2 = (int)gridDim.x - nk1p;
     const int gi = xcd_swizzle(b - nk1p, n2);
-    taa_tile<IN, kFrameTaaH, COH>(P2, T, P2.tx0 + (gi % gx) * 64, P2.ty0 + (gi / gx) * kFrameTaaH, L.Y, L.sE, L.sRP);
+    taa_tile<IN, TH, COH, NT>(P2, T, P2.tx0 + (gi % gx) * 64, P2.ty0 + (gi / gx) * TH, L.Y, L.sE, L.sRP);
     if constexpr (COH) {
         if (T.reach_dev && b == (int)gridDim.x - 1) {
             wait_all_k1_blocks(P2, T);
@@ -238,8 +245,10 @@ __device__ __forceinline__ void frame_taa_part(const Params& P2, const TaaArgs& 
         }
     }
 }
+template <int NT>
 inline int frame_taa_tiles(const Params& P) {
-    return ((P.tx1 - P.tx0 + 63) / 64) * ((P.ty1 - P.ty0 + kFrameTaaH - 1) / kFrameTaaH);
+    constexpr int TH = frame_taa_h<NT>();
+    return ((P.tx1 - P.tx0 + 63) / 64) * ((P.ty1 - P.ty0 + TH - 1) / TH);
 }
 
 }  // namespace bmfr
