@@ -407,10 +407,16 @@ def spin_up(a, cfg, local, frames, cams):
     state -- so the warm-up is this workload, and it hands over to the
     warm-up frames of the measured context without the GPU going idle
     (tools/frame_times.py: passes enqueued back to back have no slow early
-    frames).  A tiled scratch context runs without the halo exchange (its
-    results are discarded)."""
+    frames).  A tiled run spins up on an untiled context of its region's
+    size over the same rendered planes: no halo exchange to stand in for, no
+    never-written ring state read, no reach check that could stop the run."""
     if a.spin_up <= 0:
         return None
+    if cfg.tile is not None:
+        import dataclasses
+        sz = cfg.sizes()
+        cfg = dataclasses.replace(cfg, image_width=sz.region_width, image_height=sz.region_height, tile=None,
+                                  tile_halo=0)
     scratch = bmfr_amd.Denoiser(cfg, device=local)
     t0, f = time.perf_counter(), 0
     while True:
@@ -528,6 +534,9 @@ def main():
                     "kernel": ("k_fused_cols_taa<..., SAME = true>" if a.half_tmp else "k_fused_rows_taa<...>")
                               + " (K1 + K2 of the frame, one launch)",
                     "algorithmic_bytes_per_launch": fb, "launch_ms": round(r["frame_kernel_ms"], 4),
+                    "launch_ms_source": "HIP events recorded around each timed frame's launch on its stream "
+                                        "(would include any idle gap between frames; the rocprofv3 kernel-trace "
+                                        "mean of the same command is in profiles/*_kernel_stats.md)",
                     "limiter": "K1 blocks: latency of phase-1 gathers and of the fit's pivot chain, VALU issue "
                                "(roofline_k1); TAA tiles: texture path / latency (roofline_k2) -- not HBM"}
         else:
