@@ -1,4 +1,4 @@
-// image_io.cpp -- OpenEXR (scanline and tiled, NONE/RLE/ZIPS/ZIP/PIZ/PXR24) and
+// image_io.cpp -- OpenEXR (scanline and tiled, NONE/RLE/ZIPS/ZIP/PIZ/PXR24/B44/B44A) and
 // PNG I/O over zlib.  See image_io.h.  The EXR layout follows the published
 // OpenEXR 2 file format: magic + version, attribute list, per-chunk offset
 // table, chunks of (y, size, data) -- tiled files: (tile x, tile y, level x,
@@ -33,6 +33,7 @@ struct Channel {
     std::string name;
     int type;
     int xs, ys;
+    bool linear = false;  // pLinear (B44 stores such HALF samples on a log scale)
 };
 
 struct ExrHeader {
@@ -53,8 +54,8 @@ int lines_per_chunk(int compression) {
     switch (compression) {
         case BMFR_EXR_NONE: case BMFR_EXR_RLE: case BMFR_EXR_ZIPS: return 1;
         case BMFR_EXR_ZIP: case BMFR_EXR_PXR24: return 16;
-        case BMFR_EXR_PIZ: return 32;
-        default: return 0;  // B44 (6, 7), DWAA/B (8, 9): unsupported
+        case BMFR_EXR_PIZ: case BMFR_EXR_B44: case BMFR_EXR_B44A: return 32;
+        default: return 0;  // DWAA/B (8, 9): unsupported
     }
 }
 
@@ -117,7 +118,7 @@ bool parse_header(const std::vector<uint8_t>& file, ExrHeader& h, size_t& end, s
                 c.name = r.cstr();
                 if (c.name.empty()) break;
                 c.type = r.get<int32_t>();
-                r.get<uint32_t>();  // pLinear + reserved
+                c.linear = (r.get<uint32_t>() & 0xff) != 0;  // pLinear + reserved
                 c.xs = r.get<int32_t>();
                 c.ys = r.get<int32_t>();
                 h.channels.push_back(c);
@@ -153,6 +154,9 @@ bool parse_header(const std::vector<uint8_t>& file, ExrHeader& h, size_t& end, s
         return err = "bad channels / data window", false;
     for (const Channel& c : h.channels)
         if (c.xs != 1 || c.ys != 1 || c.type < 0 || c.type > 2) return err = "subsampled or unknown channel " + c.name, false;
+    if (h.compression == BMFR_EXR_B44 || h.compression == BMFR_EXR_B44A)
+        for (const Channel& c : h.channels)
+            if (c.linear && c.type == kHalf) return err = "B44 pLinear channel " + c.name + " is not supported", false;
     return true;
 }
 
@@ -580,6 +584,100 @@ bool pxr24_uncompress(const ExrHeader& h, const uint8_t* in, size_t n, int width
     return true;
 }
 
+// ------------------------------------------------------------------ B44 --
+// The published OpenEXR B44 / B44A scheme, decoder side.  The chunk holds
+// its channels one after another, each over the whole chunk: FLOAT / UINT
+// channels as their raw bytes (rows of the chunk), HALF channels as 4 x 4
+// blocks of samples, rows of blocks top to bottom.  A block is 14 bytes --
+// the first sample (mapped to an ordered 16-bit code: negative halves
+// complemented, positive ones with the top bit set), a 6-bit shift and 15
+// 6-bit differences (biased by 0x20, scaled by 2^shift) down the block's
+// first column and along each row -- or, B44A only, 3 bytes for a flat block
+// (third byte >= 13 << 2: every sample equal to the first).  Edge blocks are
+// padded; the decoder drops what lies outside the chunk.  Channels with the
+// pLinear flag (samples stored on a log scale) are rejected at the header.
+namespace b44 {
+
+void ordered_to_half(uint16_t (&s)[16]) {
+    for (uint16_t& v : s) v = (v & 0x8000) ? (uint16_t)(v & 0x7fff) : (uint16_t)~v;
+}
+
+void unpack14(const uint8_t* b, uint16_t (&s)[16]) {
+    const int shift = b[2] >> 2, bias = 0x20 << shift;
+    // (column, row) order of the differences: column 0 downwards, then each row rightwards
+    auto step = [&](int from, int r6) { return (uint16_t)(from + (r6 << shift) - bias); };
+    s[0] = (uint16_t)(b[0] << 8 | b[1]);
+    s[4] = step(s[0], ((b[2] << 4) | (b[3] >> 4)) & 0x3f);
+    s[8] = step(s[4], ((b[3] << 2) | (b[4] >> 6)) & 0x3f);
+    s[12] = step(s[8], b[4] & 0x3f);
+    s[1] = step(s[0], b[5] >> 2);
+    s[5] = step(s[4], ((b[5] << 4) | (b[6] >> 4)) & 0x3f);
+    s[9] = step(s[8], ((b[6] << 2) | (b[7] >> 6)) & 0x3f);
+    s[13] = step(s[12], b[7] & 0x3f);
+    s[2] = step(s[1], b[8] >> 2);
+    s[6] = step(s[5], ((b[8] << 4) | (b[9] >> 4)) & 0x3f);
+    s[10] = step(s[9], ((b[9] << 2) | (b[10] >> 6)) & 0x3f);
+    s[14] = step(s[13], b[10] & 0x3f);
+    s[3] = step(s[2], b[11] >> 2);
+    s[7] = step(s[6], ((b[11] << 4) | (b[12] >> 4)) & 0x3f);
+    s[11] = step(s[10], ((b[12] << 2) | (b[13] >> 6)) & 0x3f);
+    s[15] = step(s[14], b[13] & 0x3f);
+    ordered_to_half(s);
+}
+
+void unpack3(const uint8_t* b, uint16_t (&s)[16]) {
+    const uint16_t v = (uint16_t)(b[0] << 8 | b[1]);
+    for (uint16_t& x : s) x = v;
+    ordered_to_half(s);
+}
+
+bool uncompress(const ExrHeader& h, const uint8_t* in, size_t n, int width, int lines, std::vector<uint8_t>& raw) {
+    // per channel, its samples over the chunk (row-major), then interleaved per line
+    std::vector<std::vector<uint8_t>> planes;
+    size_t p = 0;
+    for (const Channel& c : h.channels) {
+        const size_t row = (size_t)width * type_bytes(c.type);
+        std::vector<uint8_t> pl(row * lines);
+        if (c.type != kHalf) {
+            if (n - p < pl.size()) return false;
+            std::memcpy(pl.data(), in + p, pl.size());
+            p += pl.size();
+        } else {
+            for (int y = 0; y < lines; y += 4)
+                for (int x = 0; x < width; x += 4) {
+                    uint16_t s[16];
+                    if (n - p < 3) return false;
+                    if (in[p + 2] >= (13 << 2)) {
+                        unpack3(in + p, s);
+                        p += 3;
+                    } else {
+                        if (n - p < 14) return false;
+                        unpack14(in + p, s);
+                        p += 14;
+                    }
+                    for (int dy = 0; dy < 4 && y + dy < lines; ++dy)
+                        for (int dx = 0; dx < 4 && x + dx < width; ++dx) {
+                            uint8_t* o = pl.data() + (size_t)(y + dy) * row + 2 * (size_t)(x + dx);
+                            o[0] = (uint8_t)(s[4 * dy + dx] & 0xff);
+                            o[1] = (uint8_t)(s[4 * dy + dx] >> 8);
+                        }
+                }
+        }
+        planes.push_back(std::move(pl));
+    }
+    if (p != n) return false;
+    uint8_t* o = raw.data();
+    for (int y = 0; y < lines; ++y)
+        for (size_t c = 0; c < planes.size(); ++c) {
+            const size_t row = (size_t)width * type_bytes(h.channels[c].type);
+            std::memcpy(o, planes[c].data() + (size_t)y * row, row);
+            o += row;
+        }
+    return true;
+}
+
+}  // namespace b44
+
 // One chunk (scanline block, or tile) of `lines` lines x `width` pixels.
 bool decode_chunk(const ExrHeader& h, const uint8_t* data, size_t size, size_t raw_size, int width, int lines,
                   std::vector<uint8_t>& raw) {
@@ -596,6 +694,8 @@ bool decode_chunk(const ExrHeader& h, const uint8_t* data, size_t size, size_t r
         return piz::uncompress(data, size, width, lines, words, raw) && raw.size() == raw_size;
     }
     if (compression == BMFR_EXR_PXR24) return pxr24_uncompress(h, data, size, width, lines, raw);
+    if (compression == BMFR_EXR_B44 || compression == BMFR_EXR_B44A)
+        return b44::uncompress(h, data, size, width, lines, raw);
     std::vector<uint8_t> t;
     if (compression == BMFR_EXR_RLE) {
         if (!rle_decode(data, size, t, raw_size)) return false;

@@ -104,11 +104,89 @@ def _pxr24(img, names, y0, lines, x0, w, half):
     return zlib.compress(bytes(out))
 
 
+def _b44_shift_round(x, shift):
+    """B44's x / 2^shift rounded to nearest, ties to even (published OpenEXR scheme)."""
+    x = x << 1
+    a = (1 << shift) - 1
+    b = (x >> (shift + 1)) & 1
+    return (x + a + b) >> (shift + 1)
+
+
+def _b44_ordered(h16: np.ndarray) -> np.ndarray:
+    """Half bit patterns -> B44's ordered 16-bit codes (inf / NaN -> 0x8000)."""
+    h = h16.astype(np.int64)
+    t = np.where(h & 0x8000, (~h) & 0xffff, h | 0x8000)
+    return np.where((h & 0x7c00) == 0x7c00, 0x8000, t)
+
+
+def _b44_block(s: np.ndarray, flat: bool):
+    """One 4x4 block (16 half bit patterns, row-major) -> (bytes, decoded bit
+    patterns).  The decoded block in closed form: t_max - (d_i << shift)."""
+    t = _b44_ordered(s)
+    tmax = int(t.max())
+    bias = 0x20
+    shift = -1
+    while True:
+        shift += 1
+        d = np.array([_b44_shift_round(tmax - int(v), shift) for v in t])
+        r = [d[0] - d[4], d[4] - d[8], d[8] - d[12],
+             d[0] - d[1], d[4] - d[5], d[8] - d[9], d[12] - d[13],
+             d[1] - d[2], d[5] - d[6], d[9] - d[10], d[13] - d[14],
+             d[2] - d[3], d[6] - d[7], d[10] - d[11], d[14] - d[15]]
+        r = [int(v) + bias for v in r]
+        if min(r) >= 0 and max(r) <= 0x3f:
+            break
+    if flat and min(r) == bias and max(r) == bias:
+        t0 = int(t[0])
+        dec = np.full(16, t0, np.int64)
+        out = bytes([t0 >> 8, t0 & 255, 0xfc])
+    else:
+        t0 = (tmax - (int(d[0]) << shift)) & 0xffff
+        dec = (tmax - (d.astype(np.int64) << shift)) & 0xffff
+        b = [t0 >> 8, t0 & 255, (shift << 2) | (r[0] >> 4), (r[0] << 4) | (r[1] >> 2), (r[1] << 6) | r[2],
+             (r[3] << 2) | (r[4] >> 4), (r[4] << 4) | (r[5] >> 2), (r[5] << 6) | r[6],
+             (r[7] << 2) | (r[8] >> 4), (r[8] << 4) | (r[9] >> 2), (r[9] << 6) | r[10],
+             (r[11] << 2) | (r[12] >> 4), (r[12] << 4) | (r[13] >> 2), (r[13] << 6) | r[14]]
+        out = bytes(v & 255 for v in b)
+    dec = np.where(dec & 0x8000, dec & 0x7fff, (~dec) & 0xffff)  # ordered code -> half bits
+    return out, dec.astype(np.uint16), shift
+
+
+B44_DECODED = {}  # channel -> {(y0, x0): half bit patterns of the chunk as B44 decodes it}
+B44_SHIFTS = []   # shift of every block written (-1: a B44A flat block)
+
+
+def _b44(img, names, y0, lines, x0, w, half, flat, types):
+    """One B44 / B44A chunk: channel after channel over the chunk; HALF
+    channels as 4x4 blocks (edge blocks padded by repeating the last row /
+    column), other channels raw."""
+    out = bytearray()
+    for n in names:
+        a = np.ascontiguousarray(img[n][y0:y0 + lines, x0:x0 + w])
+        if not types.get(n, half):
+            out += a.astype(np.float32).tobytes()
+            continue
+        h = a.astype(np.float16).view(np.uint16)
+        ph, pw = (lines + 3) // 4 * 4, (w + 3) // 4 * 4
+        hp = np.pad(h, ((0, ph - lines), (0, pw - w)), mode="edge")
+        dec = np.zeros((ph, pw), np.uint16)
+        for by in range(0, ph, 4):
+            for bx in range(0, pw, 4):
+                blk, d, sh = _b44_block(hp[by:by + 4, bx:bx + 4].reshape(16), flat)
+                B44_SHIFTS.append(-1 if len(blk) == 3 else sh)  # -1: a 3-byte flat block
+                out += blk
+                dec[by:by + 4, bx:bx + 4] = d.reshape(4, 4)
+        B44_DECODED.setdefault(n, {})[(y0, x0)] = dec[:lines, :w]
+    return bytes(out)
+
+
 RAW_CHUNKS = []  # (level, y0, lines, x0, w) of the chunks write_exr_py stored uncompressed
 
 
-def _chunk_data(img, names, dt, compression, y0, lines, x0, w, half, level=0):
-    raw = b"".join(np.ascontiguousarray(img[n][y, x0:x0 + w]).astype(dt).tobytes()
+def _chunk_data(img, names, dt, compression, y0, lines, x0, w, half, level=0, types=None):
+    types = types or {}
+    raw = b"".join(np.ascontiguousarray(img[n][y, x0:x0 + w]).astype(
+        (np.float16 if types[n] else np.float32) if n in types else dt).tobytes()
                    for y in range(y0, y0 + lines) for n in names)
     if compression == 1:
         data = _rle(_predict(raw))
@@ -118,6 +196,8 @@ def _chunk_data(img, names, dt, compression, y0, lines, x0, w, half, level=0):
         data = piz_compress(raw, w, lines, [1 if half else 2] * len(names))
     elif compression == 5:
         data = _pxr24(img, names, y0, lines, x0, w, half)
+    elif compression in (6, 7):
+        data = _b44(img, names, y0, lines, x0, w, half, compression == 7, types)
     else:
         data = raw
     if compression and len(data) >= len(raw):  # OpenEXR stores such a chunk as it is
@@ -126,15 +206,19 @@ def _chunk_data(img, names, dt, compression, y0, lines, x0, w, half, level=0):
     return data
 
 
-def write_exr_py(path, img: dict, compression: int, half: bool, tile=None, mipmap=False):
+def write_exr_py(path, img: dict, compression: int, half: bool, tile=None, mipmap=False, types=None):
     """img: channel name -> (H, W) float array.  Channels are stored sorted by
-    name.  compression 0 NONE, 1 RLE, 2 ZIPS, 3 ZIP, 4 PIZ, 5 PXR24.
+    name.  compression 0 NONE, 1 RLE, 2 ZIPS, 3 ZIP, 4 PIZ, 5 PXR24, 6 B44,
+    7 B44A.  types: channel name -> True (HALF) / False (FLOAT) where it
+    differs from `half` (B44 chunks only).
     tile = (tw, th): a tiled file (ONE_LEVEL, or MIPMAP_LEVELS round-down
     with mipmap=True: the lower levels follow level 0, box-filtered)."""
     names = sorted(img)
     H, W = img[names[0]].shape
     ptype, dt = (1, np.float16) if half else (2, np.float32)
-    chl = b"".join(n.encode() + b"\0" + struct.pack("<iIii", ptype, 0, 1, 1) for n in names) + b"\0"
+    types = types or {}
+    chl = b"".join(n.encode() + b"\0" + struct.pack("<iIii", (1 if types[n] else 2) if n in types else ptype, 0, 1, 1)
+                   for n in names) + b"\0"
     box = struct.pack("<iiii", 0, 0, W - 1, H - 1)
     version = 2 | (0x200 if tile else 0)
     hdr = (struct.pack("<II", 20000630, version) + _attr("channels", "chlist", chl) +
@@ -159,12 +243,12 @@ def write_exr_py(path, img: dict, compression: int, half: bool, tile=None, mipma
                 for tx in range((lw + tw - 1) // tw):
                     x0, y0 = tx * tw, ty * th
                     w, lines = min(tw, lw - x0), min(th, lh - y0)
-                    data = _chunk_data(im, names, dt, compression, y0, lines, x0, w, half, lv)
+                    data = _chunk_data(im, names, dt, compression, y0, lines, x0, w, half, lv, types)
                     chunks.append(struct.pack("<iiiii", tx, ty, lv, lv, len(data)) + data)
     else:
-        lpc = {0: 1, 1: 1, 2: 1, 3: 16, 4: 32, 5: 16}[compression]
+        lpc = {0: 1, 1: 1, 2: 1, 3: 16, 4: 32, 5: 16, 6: 32, 7: 32}[compression]
         for y0 in range(0, H, lpc):
-            data = _chunk_data(img, names, dt, compression, y0, min(H, y0 + lpc) - y0, 0, W, half)
+            data = _chunk_data(img, names, dt, compression, y0, min(H, y0 + lpc) - y0, 0, W, half, types=types)
             chunks.append(struct.pack("<ii", y0, len(data)) + data)
     off = len(hdr) + 8 * len(chunks)
     table = b""
@@ -390,3 +474,78 @@ def test_exr_tiled_rejects_bad_tiles(tmp_path):
     (tmp_path / "level.exr").write_bytes(bytes(b))
     assert lib().bmfr_exr_read_rgb(str(tmp_path / "level.exr").encode(), 8, 8, out.ctypes.data) != 0
     assert b"bad tile" in lib().bmfr_io_error()
+
+
+def _b44_want(shape, chunks_of, names):
+    """The decoded image of B44_DECODED's chunks, as float32, (H, W) per channel."""
+    H, W = shape
+    out = {}
+    for n in names:
+        a = np.zeros((H, W), np.uint16)
+        for (y0, x0), d in B44_DECODED[n].items():
+            a[y0:y0 + d.shape[0], x0:x0 + d.shape[1]] = d
+        out[n] = a.view(np.float16).astype(np.float32)
+    return out
+
+
+@pytest.mark.parametrize("comp", [6, 7])
+@pytest.mark.parametrize("shape,tile", [((41, 29), None), ((32, 32), None), ((3, 70), None), ((70, 2), None),
+                                        ((37, 53), (16, 8))])
+def test_exr_b44(tmp_path, comp, shape, tile):
+    """B44 / B44A (OpenImageIO reads them, bmfr.cpp:145-163): HALF channels in
+    4x4 blocks -- lossless where a block's samples differ little (shift 0),
+    rounded to 2^shift steps below the block maximum elsewhere (the closed
+    form t_max - (d << shift) of the published scheme, independent of the
+    decoder's running sums), flat blocks in 3 bytes (B44A), partial edge
+    blocks; a FLOAT channel in the same chunk is stored raw."""
+    H, W = shape
+    rng = np.random.default_rng(H * W + comp)
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    img = np.stack([1.0 + xx / 512.0,                                  # smooth: shift 0, lossless
+                    rng.normal(0, 3, (H, W)).astype(np.float32),      # noise: lossy blocks
+                    np.where(yy < H // 8 * 4, 0.5, -2.0).astype(np.float32)], -1)  # flat blocks
+    img[0, 0, 1] = np.inf
+    img[-1, -1, 1] = -0.0
+    chans = {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2], "A": rng.normal(0, 1, (H, W)).astype(np.float32)}
+    types = {"A": False}
+    path = str(tmp_path / "b44.exr")
+    B44_DECODED.clear()
+    B44_SHIFTS.clear()
+    RAW_CHUNKS.clear()
+    write_exr_py(path, chans, comp, True, tile=tile, types=types)
+    out = np.empty_like(img)
+    assert lib().bmfr_exr_read_rgb(path.encode(), W, H, out.ctypes.data) == 0, lib().bmfr_io_error()
+    want = _b44_want((H, W), B44_DECODED, "RGB")
+    for _, y0, n, x0, w in RAW_CHUNKS:  # chunks B44 would not shrink are stored as they are
+        for c, ch in enumerate("RGB"):
+            want[ch][y0:y0 + n, x0:x0 + w] = img[y0:y0 + n, x0:x0 + w, c].astype(np.float16)
+    np.testing.assert_array_equal(out[..., 0], want["R"])
+    np.testing.assert_array_equal(out[..., 1], want["G"])
+    np.testing.assert_array_equal(out[..., 2], want["B"])
+    # lossless where the scheme is: smooth and flat channels
+    np.testing.assert_array_equal(out[..., 0], img[..., 0].astype(np.float16).astype(np.float32))
+    np.testing.assert_array_equal(out[..., 2], img[..., 2].astype(np.float16).astype(np.float32))
+    # the noisy channel: lossy, each sample within half a step (2^shift of the
+    # ordered code) of its own -- measured in the ordered code, where the
+    # scheme rounds
+    g = img[..., 1].astype(np.float16)
+    fin = np.isfinite(g)
+    code = lambda a: _b44_ordered(a.view(np.uint16))  # noqa: E731
+    err = np.abs(code(out[..., 1].astype(np.float16))[fin] - code(g)[fin])
+    assert err.max() <= 1 << (max(B44_SHIFTS) - 1)
+    assert err.max() > 0 or RAW_CHUNKS
+    assert (-1 in B44_SHIFTS) == (comp == 7)  # 3-byte flat blocks: B44A only
+
+
+def test_exr_b44_rejects_plinear(tmp_path):
+    img = _img(8, 8)
+    chans = {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2]}
+    path = tmp_path / "lin.exr"
+    write_exr_py(str(path), chans, 6, True)
+    b = bytearray(path.read_bytes())
+    i = b.index(b"R\0", b.index(b"chlist"))
+    b[i + 2 + 4] = 1  # R's pLinear flag
+    path.write_bytes(bytes(b))
+    out = np.empty_like(img)
+    assert lib().bmfr_exr_read_rgb(str(path).encode(), 8, 8, out.ctypes.data) != 0
+    assert b"pLinear" in lib().bmfr_io_error()

@@ -4,8 +4,8 @@ CPU side):
 
 * the CPU restatement oracle/bmfr_oracle.c, all five stages over several
   configurations (tests/native/oracle_asan_main.c);
-* the EXR reader host/image_io.cpp (PIZ and PXR24 decoders, scanline and
-  tiled files) -- the one component that parses external files -- over a
+* the EXR reader host/image_io.cpp (PIZ, PXR24 and B44 / B44A decoders,
+  scanline and tiled files) -- the one component that parses external files -- over a
   corpus of malformed files derived from valid ones:
   every truncation length of a small file, seeded random byte corruption,
   and hand-made hostile headers (huge chunk offsets, attribute sizes past
@@ -90,6 +90,7 @@ def test_exr_reader_malformed_corpus_under_asan_ubsan(tmp_path):
     rng = np.random.default_rng(0x424D4652)
     for comp, half, tile in ((0, False, None), (1, False, None), (2, True, None), (3, False, None),
                              (4, False, None), (4, True, None), (5, False, None), (5, True, None),
+                             (6, True, None), (7, True, None), (7, True, (4, 4)),
                              (3, False, (4, 4)), (4, False, (8, 2)), (5, False, (4, 4))):
         name = f"{comp}_{int(half)}" + (f"_t{tile[0]}x{tile[1]}" if tile else "")
         src = tmp_path / f"valid_{name}.exr"
