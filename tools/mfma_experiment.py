@@ -14,7 +14,6 @@ to the reference kernels' default build (contraction on) and strict build.
 
   python tools/mfma_experiment.py [W H FRAMES [B [NB,...]]]   (B = 13 or 16)
 """
-import ctypes as C
 import json
 import os
 import sys
@@ -28,7 +27,8 @@ import torch  # noqa: E402
 
 import bmfr_amd  # noqa: E402
 import ref_run  # noqa: E402
-from bmfr_amd._lib import check, floats  # noqa: E402
+from mfma_common import load_wy, run_stages  # noqa: E402
+from bmfr_amd._lib import check  # noqa: E402
 from bmfr_amd.pipeline import _ptr  # noqa: E402
 from ref_configs import FULL_REF_CONFIGS  # noqa: E402
 
@@ -36,28 +36,9 @@ W, H, FR = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (3840, 2160
 BC = int(sys.argv[4]) if len(sys.argv) > 4 else 13
 NBS = [int(x) for x in sys.argv[5].split(",")] if len(sys.argv) > 5 else [4, 8, 16]
 rc = FULL_REF_CONFIGS.get(f"f{W}x{H}_f{BC}")
-wy = C.CDLL(os.path.join(ROOT, "tools", "libwy.so"))
-wy.wy_fitter.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_void_p, C.c_int,
-                         C.c_int]
+wy = load_wy(os.path.join(ROOT, "tools", "libwy.so"))
 cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, use_half_precision_in_tmp_data=0, library_powr=1,
                           scaled=bmfr_amd.SCALED_THIRD_ORDER if BC == 16 else bmfr_amd.SCALED_DEFAULT)
-
-
-def run_stages(sp, vp, jit, f, fitter):
-    """StagePipeline.run_stages with the fitter stage replaced by `fitter(sp, f)`."""
-    lib, h, st = sp.lib, sp.handle, torch.cuda.current_stream().cuda_stream
-    check(lib.bmfr_accumulate_noisy_data(
-        h, st, _ptr(sp.prev_pixels), _ptr(sp.accept), _ptr(sp.cur(sp.normals)), _ptr(sp.prev(sp.normals)),
-        _ptr(sp.cur(sp.positions)), _ptr(sp.prev(sp.positions)), _ptr(sp.cur(sp.noisy)), _ptr(sp.prev(sp.noisy)),
-        _ptr(sp.prev(sp.spp)), _ptr(sp.cur(sp.spp)), _ptr(sp.tmp_data), floats(vp, 16), floats(jit, 2), f), "acc")
-    fitter(sp, f)
-    check(lib.bmfr_weighted_sum(h, st, _ptr(sp.weights), _ptr(sp.mins_maxs), _ptr(sp.filtered),
-                                _ptr(sp.cur(sp.normals)), _ptr(sp.cur(sp.positions)), _ptr(sp.cur(sp.noisy)), f), "ws")
-    check(lib.bmfr_accumulate_filtered_data(
-        h, st, _ptr(sp.filtered), _ptr(sp.prev_pixels), _ptr(sp.accept), _ptr(sp.albedo), _ptr(sp.tone_mapped),
-        _ptr(sp.cur(sp.spp)), _ptr(sp.prev(sp.out)), _ptr(sp.cur(sp.out)), f), "af")
-    check(lib.bmfr_taa(h, st, _ptr(sp.prev_pixels), _ptr(sp.tone_mapped), _ptr(sp.cur(sp.result)),
-                       _ptr(sp.prev(sp.result)), f), "taa")
 
 
 def valu_fitter(sp, f):
