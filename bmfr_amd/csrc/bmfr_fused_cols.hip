@@ -152,6 +152,25 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
     }
     const float p[4] = {s01.x, s01.y, s23.x, s23.y};
     const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);  // (2u) dot == u (2 dot): same real product, one rounding
+#ifdef BMFR_FAST_FIT
+    // Experiment (not bit-exact): a - u (2 dot / |u|^2) as one fused
+    // mixed-precision FMA per element on the uniform factor RN(c2 / |u|^2)
+    // instead of upstream's RN(RN(u c2) / |u|^2) and the rounded subtraction.
+    {
+        const float sc = c2 * recip;
+#pragma unroll
+        for (int k = 0; k < kSlots / 2; ++k) {
+            float lo, hi;
+            asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel_hi:[0,0,1]" : "=v"(lo) : "v"(u[2 * k]), "v"(sc), "v"(a[k]));
+            asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+                : "=v"(hi) : "v"(u[2 * k + 1]), "v"(sc), "v"(a[k]));
+            if (k == 0 && l < c) lo = (float)a[0][0];  // rows above the pivot keep their value
+            a[k] = __builtin_convertvector((f2v{lo, hi}), h2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        return;
+    }
+#endif
     f2v q[kSlots / 2];
     if (fabsf(c2) < 0x1p100f && ulen2 >= 0x1p-100f && ulen2 < 0x1p100f) {
         const f2v vb = {ulen2, ulen2}, vy = {recip, recip};
