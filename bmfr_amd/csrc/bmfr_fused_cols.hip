@@ -221,16 +221,24 @@ __device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const float* _
     float x[kSlots];
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
+#if defined(BMFR_FAST_FIT) && BMFR_FAST_FIT >= 2
+    // Experiment (not bit-exact): the noise term in f32, one fused FMA
+    const float nf = (float)noise2;
+#define BMFR_ADD_NOISE(xv, r) __builtin_fmaf(nf, (r), (xv))
+#else
+#define BMFR_ADD_NOISE(xv, r) (float)((double)(xv) + noise2 * (double)(r))
+#endif
     if (use_pre) {  // wave-uniform
 #pragma unroll
-        for (int j = 0; j < kSlots; ++j) x[j] = (float)((double)x[j] + noise2 * (double)pre[j]);
+        for (int j = 0; j < kSlots; ++j) x[j] = BMFR_ADD_NOISE(x[j], pre[j]);
     } else if (noise) {  // wave-uniform
         float nz[kSlots];
 #pragma unroll
         for (int j = 0; j < kSlots; ++j) nz[j] = noise[l + 64 * j];
 #pragma unroll
-        for (int j = 0; j < kSlots; ++j) x[j] = (float)((double)x[j] + noise2 * (double)nz[j]);
+        for (int j = 0; j < kSlots; ++j) x[j] = BMFR_ADD_NOISE(x[j], nz[j]);
     }
+#undef BMFR_ADD_NOISE
     float p[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {

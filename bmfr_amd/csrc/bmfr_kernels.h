@@ -312,6 +312,8 @@ __device__ __forceinline__ In3<_Float16> row_next(const In3<_Float16>& v) {
     r.v.z = (uint16_t)row_next_u(v.v.z);
     return r;
 }
+// c ? a : b with both operands evaluated in every lane (cross-lane moves must
+// not end up under a partial exec mask)
 template <class T>
 __device__ __forceinline__ T pick(bool c, const T& a, const T& b) { return c ? a : b; }
 // lanes 0-31 <- lanes 32-63 (gfx950 permlane32 swap)
@@ -376,11 +378,14 @@ __device__ __forceinline__ NoisyTaps<IN> noisy_taps_issue(const Params& P, const
                 tp.over = max(max(max(vx0 - x0, x1 - (vx1 - 1)), max(vy0 - y0, y1 - (vy1 - 1))), 0);
         }
 #ifdef BMFR_TAP_SHARE
-        const bool last = (__lane_id() & 15) == 15;
-        tp.share = !last && (int)row_next_u((uint32_t)ix) == ix + 1 && (int)row_next_u((uint32_t)iy) == iy;
+        // the cross-lane moves run in every lane (no short-circuit: a move
+        // under a partial exec mask would read stale values of inactive lanes)
+        const int ixr = (int)row_next_u((uint32_t)ix), iyr = (int)row_next_u((uint32_t)iy);
+        tp.share = ((__lane_id() & 15) != 15) & (ixr == ix + 1) & (iyr == iy);
 #if BMFR_TAP_SHARE == 3
         // the wave's lanes 32-63 hold the image row below lanes 0-31 (K1's item layout)
-        tp.shareV = __lane_id() < 32 && (int)down32_u((uint32_t)ix) == ix && (int)down32_u((uint32_t)iy) == iy + 1;
+        const int ixd = (int)down32_u((uint32_t)ix), iyd = (int)down32_u((uint32_t)iy);
+        tp.shareV = (__lane_id() < 32) & (ixd == ix) & (iyd == iy + 1);
 #else
         tp.shareV = false;
 #endif
@@ -454,7 +459,7 @@ __device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const No
                 ppr = pick(tp.shareV, down32(tp.pp[0]), ppr);
                 pnr = pick(tp.shareV, down32(tp.pn[0]), pnr);
                 pci = pick(tp.shareV, down32(tp.pc[0]), pci);
-                spi = tp.shareV ? down32_u(tp.spu[0]) : spi;
+                spi = pick(tp.shareV, down32_u(tp.spu[0]), spi);
                 if (FILT) pai = pick(tp.shareV, down32(tp.pa[0]), pai);
                 r2pp = ppr, r2pn = pnr, r2pc = pci, r2sp = spi, r2pa = pai;
             }
@@ -479,7 +484,7 @@ __device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const No
                 pnr = pick(sh, row_next(bpn), pnr);
 #endif
                 pci = pick(sh, row_next(bpc), pci);
-                spi = sh ? row_next_u(bsp) : spi;
+                spi = pick(sh, row_next_u(bsp), spi);
                 if (FILT) pai = pick(sh, row_next(bpa), pai);
             }
             const f3 pp = widen(ppr), pn = widen(pnr);
