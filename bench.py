@@ -16,7 +16,9 @@ GPU: `ms_per_frame_1080p` (1920x1080) and `ms_per_frame_8k` (7680x4320, the
 1-GPU point of the north star's scaling target); BASELINE's other 4K
 configurations with their own rooflines: `ms_per_frame_cfg5` (config 5:
 half input planes, 3rd-order features, B = 16) and `ms_per_frame_f32tmp`
-(f32 tmp_data); and
+(f32 tmp_data); `ms_per_frame_fast_fit`: the headline configuration with
+bmfr_config.fast_fit (the fitter's trailing update as one fused FMA: not
+bit-exact, within 3e-6 relative L2 of the reference's strict build); and
 `ms_per_frame_sequence`: the same 4K frames through bmfr_process_sequence
 (K2 of frame f inside K1 of f + 1's launch, as the reference's frame loop
 enqueues every frame without waiting).  `value` stays the per-frame API's
@@ -106,6 +108,9 @@ def parse():
     ap.add_argument("--library-powr", action="store_true",
                     help="tone map with the device library's powr (bit-identical to the reference kernel "
                          "on gfx950) instead of the correctly rounded one")
+    ap.add_argument("--fast-fit", action="store_true",
+                    help="bmfr_config.fast_fit: the fitter's trailing update as one fused FMA (not bit-exact; "
+                         "within 3e-6 rel-L2 of the reference's strict build, tests/test_gpu_fast_fit.py)")
     ap.add_argument("--no-1080p", action="store_true", help="skip the 1920x1080 line (N = 1 only)")
     ap.add_argument("--spin-up", type=float, default=1.0,
                     help="seconds of untimed frames (a scratch context) before each measured run (clock ramp)")
@@ -189,7 +194,8 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, scaled=scaled,
                               use_half_precision_in_tmp_data=a.half_tmp,
                               tile=tile if grid else None, tile_halo=a.halo if grid else 0,
-                              input_half=int(a.input_half), library_powr=int(a.library_powr))
+                              input_half=int(a.input_half), library_powr=int(a.library_powr),
+                              fast_fit=int(a.fast_fit))
     local = dev.index
     den = bmfr_amd.Denoiser(cfg, device=local)
     region = den.region
@@ -490,8 +496,9 @@ def main():
     rvar = {}
     if world == 1 and not a.no_variants and not a.sequence:
         import copy
-        for key, upd in (("cfg5", dict(third_order=True, input_half=True, half_tmp=1)),
-                         ("f32tmp", dict(third_order=False, input_half=False, half_tmp=0))):
+        for key, upd in (("cfg5", dict(third_order=True, input_half=True, half_tmp=1, fast_fit=False)),
+                         ("f32tmp", dict(third_order=False, input_half=False, half_tmp=0, fast_fit=False)),
+                         ("fast_fit", dict(third_order=False, input_half=False, half_tmp=1, fast_fit=True))):
             if all(getattr(a, k) == v for k, v in upd.items()):
                 continue  # the main line already is this configuration
             b = copy.copy(a)
@@ -510,7 +517,8 @@ def main():
     s = 2 if a.input_half else 4
     tile_px = tile[2] * tile[3]
     tmp = "half" if a.half_tmp else "f32"
-    workload = f"bmfr_{W}x{H}_B{cfg.buffer_count}_{tmp}tmp" + ("_f16in" if a.input_half else "")
+    workload = f"bmfr_{W}x{H}_B{cfg.buffer_count}_{tmp}tmp" + ("_f16in" if a.input_half else "") + \
+        ("_fastfit" if a.fast_fit else "")
     ms_per_frame = r["ms_per_frame"]
     if rank == 0:
         achieved = k1_bytes_per_px(s) * tile_px / (r["k1_ms"] * 1e-3) / 1e9
@@ -558,7 +566,9 @@ def main():
             "data": "synthetic (GPU-rendered 1-spp frames + features, resident in HBM)",
             "config": {"workload": workload, "image": f"{W}x{H}", "buffer_count": cfg.buffer_count,
                        "half_tmp_data": a.half_tmp, "input_half": int(a.input_half),
-                       "powr": "device library" if a.library_powr else "correctly rounded", "frames_timed": a.steps,
+                       "powr": "device library" if a.library_powr else "correctly rounded",
+                       "fit": "fused trailing update (fast_fit)" if a.fast_fit else "exact (reference strict build)",
+                       "frames_timed": a.steps,
                        "frames_pipelined": world == 1 and a.sequence,
                        "parallelism": (f"tiles {tx}x{ty}, halo {a.halo} px, "
                                        f"{'RCCL' if backend == 'nccl' else backend} halo exchange"
@@ -597,7 +607,7 @@ def main():
         for key, (b, rv) in rvar.items():
             vs = 2 if b.input_half else 4
             wl = f"bmfr_{W}x{H}_B{rv['cfg'].buffer_count}_{'half' if b.half_tmp else 'f32'}tmp" + \
-                 ("_f16in" if b.input_half else "")
+                 ("_f16in" if b.input_half else "") + ("_fastfit" if b.fast_fit else "")
             line[f"ms_per_frame_{key}"] = variant_line(rv, vs, W, H, wl, "k_fused_cols_taa<..., SAME = true>"
                                                        if b.half_tmp else "k_fused_rows_taa<...>")
         if world == 1 and a.cpu_frames > 0:

@@ -27,8 +27,29 @@ def _deps_mtime() -> float:
     return max(os.path.getmtime(f) for f in files)
 
 
+class _BuildLock:
+    """One build at a time across processes (pytest-xdist workers may all
+    find a library stale at once and would race on the same object files)."""
+
+    def __enter__(self):
+        import fcntl
+        self.f = open(os.path.join(HERE, ".build.lock"), "w")
+        fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+        fcntl.flock(self.f, fcntl.LOCK_UN)
+        self.f.close()
+
+
 def build(force: bool = False, verbose: bool = False, diag: bool = False, variant: str = "",
           extra_flags=()) -> str:
+    with _BuildLock():
+        return _build(force, verbose, diag, variant, extra_flags)
+
+
+def _build(force, verbose, diag, variant, extra_flags) -> str:
     """Build libbmfr.so (or, diag=True, libbmfr_diag.so: same library with
     in-kernel phase timestamps compiled in, for profiling only; or, with
     variant=NAME, libbmfr_NAME.so built with extra_flags, for A/B timing --
@@ -66,6 +87,11 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     and the bmfr_host program (host/bmfr_host.cpp, the reference's bmfr.cpp
     on libbmfr), next to libbmfr.so (rpath $ORIGIN)."""
     build(verbose=verbose)
+    with _BuildLock():
+        return _build_host(force, verbose)
+
+
+def _build_host(force, verbose) -> str:
     srcs = [os.path.join(HOST_DIR, f) for f in os.listdir(HOST_DIR)]
     newest = max(os.path.getmtime(f) for f in srcs + [LIB])
     steps = [

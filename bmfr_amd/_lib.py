@@ -54,6 +54,7 @@ class Config(C.Structure):
         ("tile_halo", C.c_int),
         ("input_half", C.c_int),
         ("library_powr", C.c_int),
+        ("fast_fit", C.c_int),
     ]
 
 

@@ -160,6 +160,7 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     P.half_tmp = c->use_half_precision_in_tmp_data ? 1 : 0;
     P.input_half = c->input_half ? 1 : 0;
     P.library_powr = c->library_powr ? 1 : 0;
+    P.fast_fit = c->fast_fit ? 1 : 0;
     P.ox = s->region_x;
     P.oy = s->region_y;
     P.stride = s->region_width;

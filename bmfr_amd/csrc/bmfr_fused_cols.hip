@@ -138,7 +138,7 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // 4si, 4si+1 of one step feed chains 0, 1 together) run as two packed pairs,
 // and the quotients as packed Markstein steps.  Every lane of a packed op
 // rounds like the scalar op.
-template <int c>
+template <int c, bool FAST = false>
 __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
                                               int l) {
     f2v s01 = {0.f, 0.f}, s23 = {0.f, 0.f};
@@ -152,11 +152,12 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
     }
     const float p[4] = {s01.x, s01.y, s23.x, s23.y};
     const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);  // (2u) dot == u (2 dot): same real product, one rounding
-#ifdef BMFR_FAST_FIT
-    // Experiment (not bit-exact): a - u (2 dot / |u|^2) as one fused
-    // mixed-precision FMA per element on the uniform factor RN(c2 / |u|^2)
-    // instead of upstream's RN(RN(u c2) / |u|^2) and the rounded subtraction.
-    {
+    if constexpr (FAST) {
+        // bmfr_config.fast_fit (not bit-exact): a - u (2 dot / |u|^2) as one
+        // fused mixed-precision FMA per element on the uniform factor
+        // RN(c2 / |u|^2), instead of upstream's RN(a - RN(RN(u c2) / |u|^2))
+        // -- one rounding (to f32, then half as upstream) where upstream has
+        // three; the dot product stays upstream's.
         const float sc = c2 * recip;
 #pragma unroll
         for (int k = 0; k < kSlots / 2; ++k) {
@@ -170,7 +171,6 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
         __builtin_amdgcn_sched_barrier(0);
         return;
     }
-#endif
     f2v q[kSlots / 2];
     if (fabsf(c2) < 0x1p100f && ulen2 >= 0x1p-100f && ulen2 < 0x1p100f) {
         const f2v vb = {ulen2, ulen2}, vy = {recip, recip};
@@ -221,13 +221,7 @@ __device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const float* _
     float x[kSlots];
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
-#if defined(BMFR_FAST_FIT) && BMFR_FAST_FIT >= 2
-    // Experiment (not bit-exact): the noise term in f32, one fused FMA
-    const float nf = (float)noise2;
-#define BMFR_ADD_NOISE(xv, r) __builtin_fmaf(nf, (r), (xv))
-#else
 #define BMFR_ADD_NOISE(xv, r) (float)((double)(xv) + noise2 * (double)(r))
-#endif
     if (use_pre) {  // wave-uniform
 #pragma unroll
         for (int j = 0; j < kSlots; ++j) x[j] = BMFR_ADD_NOISE(x[j], pre[j]);
@@ -357,7 +351,7 @@ __device__ __forceinline__ void k1_barrier() { lds_barrier(); }
 // implicit.  W is a run-time (wave-uniform) value, so the NW waves run one
 // copy of the code: column ownership is a scalar branch, while the slot of
 // every column a step touches is known at compile time.
-template <int NS, int FS, int NW = 4>
+template <int NS, int FS, int NW = 4, bool FAST = false>
 struct WaveFit {
     static constexpr int B = NS + FS + 3;
     static constexpr int NF = B - 3;  // pivot columns
@@ -410,7 +404,7 @@ struct WaveFit {
                 const float ulen2 = L.piv[c % kUBufs][0], recip = L.piv[c % kUBufs][1];
                 if constexpr (nxt < NF) {
                     if (publish) {  // the next pivot is every wave's critical path: issue it first
-                        update_column<c>(a[slot(nxt)], u, ulen2, recip, l);
+                        update_column<c, FAST>(a[slot(nxt)], u, ulen2, recip, l);
                         publish_pivot<nxt, B>(a[slot(nxt)], L, l);
                     }
                 }
@@ -419,7 +413,7 @@ struct WaveFit {
                     const int fb = 1 + W + NW * k;
                     if constexpr (NW * k + NW > c) {  // slot k holds columns <= NW k + NW
                         if (owns(W, fb) && fb > c && !(publish && fb == nxt))
-                            update_column<c>(a[k], u, ulen2, recip, l);
+                            update_column<c, FAST>(a[k], u, ulen2, recip, l);
                     }
                 });
             }
@@ -592,7 +586,7 @@ constexpr int kColsWaves = 4;  // minimum waves per SIMD for the register alloca
 // COH: the TAA tiles of the same frame run in this launch: the accumulated
 // colour and the reprojected positions they read are stored device-coherent
 // and the block publishes done[g] = epoch once they are.
-template <int NS, int FS, class IN, bool COH = false, int NW = 4>
+template <int NS, int FS, class IN, bool COH = false, int NW = 4, bool FAST = false>
 __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, Lds<NS + FS + 3, NW>& L, int g) {
     constexpr int B = NS + FS + 3;
     constexpr int NT = 64 * NW, NI = 16 / NW;  // threads; items (rows) per thread
@@ -679,14 +673,14 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     }
     report_reach(P, A.reach, over);
     float pre[kPre][kSlots];
-    WaveFit<NS, FS, NW>::prefetch_noise(w, l, A.noise, pre);
+    WaveFit<NS, FS, NW, FAST>::prefetch_noise(w, l, A.noise, pre);
     k1_barrier();  // matrix in LDS; phase 1's global stores drain in the background
     BMFR_STAMP(1);
     BMFR_STAMP(2);  // scaling runs inside the per-wave fit
 
     // ---- fit: min/max scaling, Householder QR, right-hand side ----
     if (t == 0) L.delay = P.debug_delay;  // read after the fit's barriers
-    WaveFit<NS, FS, NW>::run(L, w, l, A.noise, pre, P.noise2, P.max_polls, kp);
+    WaveFit<NS, FS, NW, FAST>::run(L, w, l, A.noise, pre, P.noise2, P.max_polls, kp);
     // Phase 3's loads (normal and position of the NI items, bmfr.cl:725-729)
     // go out now: they land while wave 0 back-substitutes and the others wait.
     int l3 = l;  // opaque copy: recompute phase-1 addresses instead of keeping them live across the fit
@@ -825,10 +819,11 @@ constexpr int kMinWavesSimd = BMFR_K1_MIN_WAVES;
 constexpr int kMinWavesSimd = kNW == 4 ? 4 : 6;
 #endif
 
-template <int NS, int FS, class IN>
+// FAST: bmfr_config.fast_fit (the fused trailing update, update_column).
+template <int NS, int FS, class IN, bool FAST = false>
 __global__ __launch_bounds__(kK1Threads, kMinWavesSimd) void k_fused_cols(Params P, K1Args A) {
     __shared__ Lds<NS + FS + 3, kNW> L;
-    k1_cols_body<NS, FS, IN, false, kNW>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
+    k1_cols_body<NS, FS, IN, false, kNW, FAST>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
 }
 
 // K1 and K2 (64 x kFrameTaaH tiles) in one launch: work-groups [0, nk1) are K1
@@ -844,7 +839,7 @@ __global__ __launch_bounds__(kK1Threads, kMinWavesSimd) void k_fused_cols(Params
 //     their outputs device-coherent.  Work-groups of one XCD are dispatched
 //     in order, so every K1 block a waiting tile needs has been dispatched:
 //     the waits end.
-template <int NS, int FS, class IN, bool SAME = false>
+template <int NS, int FS, class IN, bool SAME = false, bool FAST = false>
 __global__ __launch_bounds__(kK1Threads, kMinWavesSimd) void k_fused_cols_taa(Params P, K1Args A, Params P2,
                                                                               TaaArgs T, int nk1, int nk1p) {
     __shared__ union {
@@ -852,7 +847,7 @@ __global__ __launch_bounds__(kK1Threads, kMinWavesSimd) void k_fused_cols_taa(Pa
         FrameTaaLds<kK1Threads> k2;
     } U;
     const int b = blockIdx.x;
-    if (b < nk1) k1_cols_body<NS, FS, IN, SAME, kNW>(P, A, U.k1, xcd_swizzle(b, nk1));
+    if (b < nk1) k1_cols_body<NS, FS, IN, SAME, kNW, FAST>(P, A, U.k1, xcd_swizzle(b, nk1));
     else if (b >= nk1p) frame_taa_part<IN, SAME, kK1Threads>(P2, T, b, nk1p, U.k2);
 }
 
@@ -860,11 +855,26 @@ __global__ __launch_bounds__(kK1Threads, kMinWavesSimd) void k_fused_cols_taa(Pa
 
 bool fused_cols_supported(const Params& P) { return P.half_tmp && fused_supported(P); }
 
-template <int FS, class IN>
-static void launch_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
-    hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN>), dim3(k1_blocks(P)), dim3(cols::kK1Threads), 0, st, P,
-                       k1_args(A));
+// The column-split kernels' template arguments from the run-time parameters:
+// FS (6 or 9 scaled features), the input element type, fast_fit.
+template <template <int, class, bool> class L, class... Args>
+static void dispatch_cols(const Params& Q, Args&&... args) {
+    if (Q.scaled == 6) {
+        if (Q.input_half) Q.fast_fit ? L<6, _Float16, true>::go(args...) : L<6, _Float16, false>::go(args...);
+        else Q.fast_fit ? L<6, float, true>::go(args...) : L<6, float, false>::go(args...);
+    } else {
+        if (Q.input_half) Q.fast_fit ? L<9, _Float16, true>::go(args...) : L<9, _Float16, false>::go(args...);
+        else Q.fast_fit ? L<9, float, true>::go(args...) : L<9, float, false>::go(args...);
+    }
 }
+
+template <int FS, class IN, bool FAST>
+struct LaunchCols {
+    static void go(const Params& P, hipStream_t st, const FusedArgs& A) {
+        hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, FAST>), dim3(k1_blocks(P)), dim3(cols::kK1Threads), 0, st,
+                           P, k1_args(A));
+    }
+};
 
 bool seq_fused_supported(const Params& P) { return fused_cols_supported(P) && P.ring == 0; }
 // Untiled frames, a tiled context's whole frame and its border launch (the
@@ -872,43 +882,43 @@ bool seq_fused_supported(const Params& P) { return fused_cols_supported(P) && P.
 // report).
 bool frame_fused_supported(const Params& P) { return fused_supported(P); }
 
-template <int FS, class IN>
-static void launch_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
-    const int nk1 = P.ring < 0 || P.nbx <= 0 || P.nby <= 0 ? 0 : k1_blocks(P), nk1p = (nk1 + 7) & ~7;
-    const int nk2 = frame_taa_tiles<cols::kK1Threads>(P);
-    hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN, true>), dim3(nk1p + nk2), dim3(cols::kK1Threads), 0, st,
-                       P, k1_args(A), P, taa_args(A), nk1, nk1p);
-}
+template <int FS, class IN, bool FAST>
+struct LaunchFrameOne {
+    static void go(const Params& P, hipStream_t st, const FusedArgs& A) {
+        const int nk1 = P.ring < 0 || P.nbx <= 0 || P.nby <= 0 ? 0 : k1_blocks(P), nk1p = (nk1 + 7) & ~7;
+        const int nk2 = frame_taa_tiles<cols::kK1Threads>(P);
+        hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN, true, FAST>), dim3(nk1p + nk2), dim3(cols::kK1Threads),
+                           0, st, P, k1_args(A), P, taa_args(A), nk1, nk1p);
+    }
+};
 
 hipError_t launch_fused_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
     if (!fused_cols_supported(P)) return launch_fused_rows_frame_one(P, st, A);  // f32 tmp_data
-    if (P.scaled == 6) P.input_half ? launch_frame_one<6, _Float16>(P, st, A) : launch_frame_one<6, float>(P, st, A);
-    else P.input_half ? launch_frame_one<9, _Float16>(P, st, A) : launch_frame_one<9, float>(P, st, A);
+    dispatch_cols<LaunchFrameOne>(P, P, st, A);
     return hipGetLastError();
 }
 
-template <int FS, class IN>
-static void launch_cols_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
-                            const FusedArgs* A2) {
-    const int nk1 = A ? k1_blocks(P) : 0, nk1p = (nk1 + 7) & ~7;
-    const int nk2 = A2 ? frame_taa_tiles<cols::kK1Threads>(P2) : 0;
-    if (nk1 + nk2 == 0) return;
-    const TaaArgs T = A2 ? taa_args(*A2) : TaaArgs{};
-    hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN>), dim3(nk2 ? nk1p + nk2 : nk1), dim3(cols::kK1Threads), 0,
-                       st, A ? P : P2, k1_args(A ? *A : *A2), A2 ? P2 : P, T, nk1, nk1p);
-}
+template <int FS, class IN, bool FAST>
+struct LaunchColsTaa {
+    static void go(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2, const FusedArgs* A2) {
+        const int nk1 = A ? k1_blocks(P) : 0, nk1p = (nk1 + 7) & ~7;
+        const int nk2 = A2 ? frame_taa_tiles<cols::kK1Threads>(P2) : 0;
+        if (nk1 + nk2 == 0) return;
+        const TaaArgs T = A2 ? taa_args(*A2) : TaaArgs{};
+        hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN, false, FAST>), dim3(nk2 ? nk1p + nk2 : nk1),
+                           dim3(cols::kK1Threads), 0, st, A ? P : P2, k1_args(A ? *A : *A2), A2 ? P2 : P, T, nk1,
+                           nk1p);
+    }
+};
 
 hipError_t launch_fused_k1_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
                                const FusedArgs* A2) {
-    const Params& Q = A ? P : P2;
-    if (Q.scaled == 6) Q.input_half ? launch_cols_taa<6, _Float16>(P, st, A, P2, A2) : launch_cols_taa<6, float>(P, st, A, P2, A2);
-    else Q.input_half ? launch_cols_taa<9, _Float16>(P, st, A, P2, A2) : launch_cols_taa<9, float>(P, st, A, P2, A2);
+    dispatch_cols<LaunchColsTaa>(A ? P : P2, P, st, A, P2, A2);
     return hipGetLastError();
 }
 
 hipError_t launch_fused_k1_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
-    if (P.scaled == 6) P.input_half ? launch_cols<6, _Float16>(P, st, A) : launch_cols<6, float>(P, st, A);
-    else P.input_half ? launch_cols<9, _Float16>(P, st, A) : launch_cols<9, float>(P, st, A);
+    dispatch_cols<LaunchCols>(P, P, st, A);
     return hipGetLastError();
 }
 

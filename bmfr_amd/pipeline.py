@@ -52,6 +52,9 @@ class BmfrConfig:
     # Tone map powr: 0 = correctly rounded (== the CPU oracle), 1 = the device
     # library's powr (== the reference kernel on gfx950) (include/bmfr.h: library_powr)
     library_powr: int = 0
+    # Householder trailing update as one fused FMA (not bit-exact, within 3e-6 rel-L2 of the
+    # reference's strict build; column-split K1 only) (include/bmfr.h: fast_fit)
+    fast_fit: int = 0
 
     @property
     def buffer_count(self) -> int:
@@ -78,6 +81,7 @@ class BmfrConfig:
             c.tile_halo = self.tile_halo
         c.input_half = self.input_half
         c.library_powr = self.library_powr
+        c.fast_fit = self.fast_fit
         return c
 
     def sizes(self) -> _lib.Sizes:

@@ -117,6 +117,16 @@ typedef struct bmfr_config {
      * kernel compiled for gfx950 computes (one in four results 1 ulp from
      * the correctly rounded one), ~130 instructions. */
     int library_powr;
+    /* Householder trailing update of the fitter (bmfr.cl:606-655), each
+     * element's t - 2 u dot / |u|^2: 0 (default) = upstream's roundings (u * c,
+     * then / |u|^2, then the subtraction; the output equals the reference's
+     * strict build bit for bit); 1 = one fused multiply-add on the block-wide
+     * factor 2 dot / |u|^2, no longer bit-exact: TAA output within 3e-6
+     * relative L2 of the reference's strict build and 1.3e-5 of its default
+     * build at 3840x2160 (the two reference builds differ by ~1.2e-5), ~9 %
+     * less K1 time.  Applies to the column-split K1 (canonical feature lists,
+     * half tmp_data, every frame API); other paths run the exact update. */
+    int fast_fit;
 } bmfr_config;
 
 /* Sizes derived from a config (bmfr.cpp:104-118, 316-343). */

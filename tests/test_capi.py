@@ -136,7 +136,7 @@ def test_synth_frame_properties():
 
 
 def test_config_struct_matches_header():
-    """The ctypes mirror of bmfr_config has the header's size (input_half is the last field)."""
+    """The ctypes mirror of bmfr_config has the header's size (fast_fit is the last field)."""
     import subprocess
     import tempfile
     src = '#include <stdio.h>\n#include "bmfr.h"\nint main(void){printf("%zu %zu", sizeof(bmfr_config), ' \
