@@ -287,49 +287,8 @@ struct NoisyTaps {
     uint32_t inb;  // bit i: tap i inside the image
     float pfx, pfy, flx, fly;
     int over;
-#ifdef BMFR_TAP_SHARE
-    bool share;   // taps 1 and 3 are the next lane's taps 0 and 2 (not loaded here)
-    bool shareV;  // (BMFR_TAP_SHARE == 3, lanes 0-31) tap 2 is lane l + 32's tap 0
-#endif
 };
 
-#ifdef BMFR_TAP_SHARE
-// Tap sharing between neighbouring lanes (experiment, -DBMFR_TAP_SHARE):
-// lane l's right-hand taps (ix + 1, iy) and (ix + 1, iy + 1) are lane l + 1's
-// left-hand taps when lane l + 1 reprojects to (ix + 1, iy) -- the same
-// clamped addresses, so the same values.  Such lanes skip those loads and
-// take the values by one DPP move within the 16-lane row (row_shl:1; the
-// row's last lane always loads).
-__device__ __forceinline__ uint32_t row_next_u(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x101, 0xf, 0xf, false);
-}
-__device__ __forceinline__ float row_next_f(float v) { return __uint_as_float(row_next_u(__float_as_uint(v))); }
-__device__ __forceinline__ f3 row_next(const f3& v) { return f3{row_next_f(v.x), row_next_f(v.y), row_next_f(v.z)}; }
-__device__ __forceinline__ In3<float> row_next(const In3<float>& v) { return In3<float>{row_next(v.v)}; }
-__device__ __forceinline__ In3<_Float16> row_next(const In3<_Float16>& v) {
-    In3<_Float16> r;
-    r.v.xy = row_next_u(v.v.xy);
-    r.v.z = (uint16_t)row_next_u(v.v.z);
-    return r;
-}
-// c ? a : b with both operands evaluated in every lane (cross-lane moves must
-// not end up under a partial exec mask)
-template <class T>
-__device__ __forceinline__ T pick(bool c, const T& a, const T& b) { return c ? a : b; }
-// lanes 0-31 <- lanes 32-63 (gfx950 permlane32 swap)
-__device__ __forceinline__ uint32_t down32_u(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_permlane32_swap((int)v, (int)v, false, false)[1];
-}
-__device__ __forceinline__ float down32_f(float v) { return __uint_as_float(down32_u(__float_as_uint(v))); }
-__device__ __forceinline__ f3 down32(const f3& v) { return f3{down32_f(v.x), down32_f(v.y), down32_f(v.z)}; }
-__device__ __forceinline__ In3<float> down32(const In3<float>& v) { return In3<float>{down32(v.v)}; }
-__device__ __forceinline__ In3<_Float16> down32(const In3<_Float16>& v) {
-    In3<_Float16> r;
-    r.v.xy = down32_u(v.v.xy);
-    r.v.z = (uint16_t)down32_u(v.v.z);
-    return r;
-}
-#endif
 
 template <bool FILT = false, class IN = float>
 __device__ __forceinline__ NoisyTaps<IN> noisy_taps_issue(const Params& P, const NoisyInputs& in, const Camera& cam,
@@ -377,36 +336,13 @@ __device__ __forceinline__ NoisyTaps<IN> noisy_taps_issue(const Params& P, const
             if (x0 <= x1 && y0 <= y1)
                 tp.over = max(max(max(vx0 - x0, x1 - (vx1 - 1)), max(vy0 - y0, y1 - (vy1 - 1))), 0);
         }
-#ifdef BMFR_TAP_SHARE
-        // the cross-lane moves run in every lane (no short-circuit: a move
-        // under a partial exec mask would read stale values of inactive lanes)
-        const int ixr = (int)row_next_u((uint32_t)ix), iyr = (int)row_next_u((uint32_t)iy);
-        tp.share = ((__lane_id() & 15) != 15) & (ixr == ix + 1) & (iyr == iy);
-#if BMFR_TAP_SHARE == 3
-        // the wave's lanes 32-63 hold the image row below lanes 0-31 (K1's item layout)
-        const int ixd = (int)down32_u((uint32_t)ix), iyd = (int)down32_u((uint32_t)iy);
-        tp.shareV = (__lane_id() < 32) & (ixd == ix) & (iyd == iy + 1);
-#else
-        tp.shareV = false;
-#endif
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int sx = ix + (i & 1), sy = iy + (i >> 1);
             tp.inb |= (uint32_t)(sx >= 0 && sy >= 0 && sx < P.width && sy < P.height) << i;
             const uint32_t s = pix(P, clamp_rx(P, sx), clamp_ry(P, sy));
-#if defined(BMFR_TAP_SHARE) && BMFR_TAP_SHARE == 2  // colours only: positions / normals always loaded
             tp.pp[i] = ld3raw<IN>(in.p_prev, s);
             tp.pn[i] = ld3raw<IN>(in.n_prev, s);
-            if ((i & 1) && tp.share) continue;
-#else
-#ifdef BMFR_TAP_SHARE
-            if ((i & 1) && tp.share) continue;
-            if (i == 2 && tp.shareV) continue;
-#endif
-            tp.pp[i] = ld3raw<IN>(in.p_prev, s);
-            tp.pn[i] = ld3raw<IN>(in.n_prev, s);
-#endif
             tp.pc[i] = ld3(in.noisy_prev, s);
             tp.spu[i] = ld_px(in.spp_prev, s);
             if (FILT) tp.pa[i] = ld3(acc_prev, s);  // same taps (bmfr.cl:801-832)
@@ -435,65 +371,12 @@ __device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const No
     float tap_total = 0.f;
     if (frame > 0) {
         float total = 0.f;
-#if BMFR_TAP_SHARE == 3
-        In3<IN> r2pp, r2pn;  // tap 2 as resolved (tap 3 of the previous lane takes it)
-        f3 r2pc, r2pa;
-        uint32_t r2sp;
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {  // bmfr.cl:374-419
-#ifdef BMFR_TAP_SHARE
-            // a sharing lane's right-hand taps: the next lane's left-hand ones
-            // (as that lane resolved them); with shareV, tap 2 is lane l + 32's tap 0
-            const bool sh = (i & 1) && tp.share;
-            const int k = (i & 1) ? i - 1 : i;
-#if BMFR_TAP_SHARE == 2
-            const In3<IN>&ppr = tp.pp[i], &pnr = tp.pn[i];
-#else
-            In3<IN> ppr = tp.pp[i], pnr = tp.pn[i];
-#endif
-            f3 pci = tp.pc[i], pai = FILT ? tp.pa[i] : f3{0.f, 0.f, 0.f};
-            uint32_t spi = tp.spu[i];
-#if BMFR_TAP_SHARE == 3
-            if (i == 2) {
-                ppr = pick(tp.shareV, down32(tp.pp[0]), ppr);
-                pnr = pick(tp.shareV, down32(tp.pn[0]), pnr);
-                pci = pick(tp.shareV, down32(tp.pc[0]), pci);
-                spi = pick(tp.shareV, down32_u(tp.spu[0]), spi);
-                if (FILT) pai = pick(tp.shareV, down32(tp.pa[0]), pai);
-                r2pp = ppr, r2pn = pnr, r2pc = pci, r2sp = spi, r2pa = pai;
-            }
-#endif
-            {
-#if BMFR_TAP_SHARE == 3
-                // tap 3 from the next lane's resolved tap 2
-                const In3<IN>& bpp = i == 3 ? r2pp : tp.pp[k];
-                const In3<IN>& bpn = i == 3 ? r2pn : tp.pn[k];
-                const f3& bpc = i == 3 ? r2pc : tp.pc[k];
-                const uint32_t bsp = i == 3 ? r2sp : tp.spu[k];
-                const f3& bpa = i == 3 ? r2pa : tp.pa[k];
-#else
-                const In3<IN>& bpp = tp.pp[k];
-                const In3<IN>& bpn = tp.pn[k];
-                const f3& bpc = tp.pc[k];
-                const uint32_t bsp = tp.spu[k];
-                const f3& bpa = tp.pa[k];
-#endif
-#if BMFR_TAP_SHARE != 2
-                ppr = pick(sh, row_next(bpp), ppr);
-                pnr = pick(sh, row_next(bpn), pnr);
-#endif
-                pci = pick(sh, row_next(bpc), pci);
-                spi = pick(sh, row_next_u(bsp), spi);
-                if (FILT) pai = pick(sh, row_next(bpa), pai);
-            }
-            const f3 pp = widen(ppr), pn = widen(pnr);
-#else
             const f3 pp = widen(tp.pp[i]), pn = widen(tp.pn[i]);
             const f3& pci = tp.pc[i];
             const uint32_t spi = tp.spu[i];
             const f3& pai = tp.pa[i];
-#endif
             const f3 d{pp.x - wp.x, pp.y - wp.y, pp.z - wp.z};
             const f3 dn{pn.x - nrm.x, pn.y - nrm.y, pn.z - nrm.z};
             if ((tp.inb & (1u << i)) && dot3(d, d) < P.position_limit_sq && dot3(dn, dn) < P.normal_limit_sq) {
