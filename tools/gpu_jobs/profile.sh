@@ -10,7 +10,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:-prof}
-W=${2:-3840}; H=${3:-2160}; shift 3 2>/dev/null; X="$*"
+W=${2:-3840}; H=${3:-2160}; shift $(( $# < 3 ? $# : 3 )); X="$*"
 mkdir -p $O
 P="python3 tools/k1_frames.py $W $H 12 $X"
 F="python3 tools/frame_times.py $W $H 12 $X"

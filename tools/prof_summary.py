@@ -82,8 +82,8 @@ def pmc(d, counter):
 
 
 # K1 / K2 of the default configuration; K1_NAME / K2_NAME select another one
-# (e.g. "k_fused_cols<4, 9, _Float16>" / "k_fused_taa<_Float16>" for config 5).
-KERNELS = {"K1 k_fused_cols": os.environ.get("K1_NAME", "k_fused_cols<4, 6, float>"),
+# (config 5: the mangled names "_ZN4bmfr4cols12k_fused_colsILi4ELi9EDF16_Lb0E" / "_ZN4bmfr11k_fused_taaIDF16_E").
+KERNELS = {"K1 k_fused_cols": os.environ.get("K1_NAME", "k_fused_cols<4, 6, float, false>"),
            "K2 k_fused_taa": os.environ.get("K2_NAME", "k_fused_taa<float>")}
 
 
