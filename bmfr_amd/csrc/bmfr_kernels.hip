@@ -111,8 +111,14 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
 // Tile height measured at 4K (K2 ms): 8: 0.114, 12: 0.105, 16: 0.112,
 // 24: 0.130, 32: 0.135; forcing 4 waves/SIMD (128 VGPRs) at 16: 0.159.
 constexpr int kTaaW = 64, kTaaH = 12;
+// Threads per tile (experiment: -DBMFR_K2_NT=384 / 768 -- 2 / 1 output
+// pixels per thread instead of 3, fewer registers, more waves per SIMD).
+#ifndef BMFR_K2_NT
+#define BMFR_K2_NT 256
+#endif
+constexpr int kTaaNT = BMFR_K2_NT;
 template <class IN>
-__global__ __launch_bounds__(256) void k_fused_taa(Params P, TaaArgs T) {
+__global__ __launch_bounds__(kTaaNT) void k_fused_taa(Params P, TaaArgs T) {
     __shared__ float4 Y[(kTaaW + 2) * (kTaaH + 2)];  // YCoCg (+ pad): one 16-byte read per neighbour
     __shared__ double sE[kPowrENum];
     __shared__ double2 sRP[kPowrRPNum];
@@ -121,7 +127,7 @@ __global__ __launch_bounds__(256) void k_fused_taa(Params P, TaaArgs T) {
     const int gi = xcd_swizzle(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int bxi = gi % gridDim.x, byi = gi / gridDim.x;
     forward_reach(T, blockIdx.x == 0 && blockIdx.y == 0);
-    taa_tile<IN, kTaaH>(P, T, P.tx0 + bxi * kTaaW, P.ty0 + byi * kTaaH, Y, sE, sRP);
+    taa_tile<IN, kTaaH, false, kTaaNT>(P, T, P.tx0 + bxi * kTaaW, P.ty0 + byi * kTaaH, Y, sE, sRP);
 }
 
 // ------------------------------------------------------------ halo copy --
@@ -268,8 +274,8 @@ hipError_t launch_fused_k1_blocks(const Params& P, hipStream_t st, const FusedAr
 
 hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A) {
     const dim3 grd((P.tx1 - P.tx0 + kTaaW - 1) / kTaaW, (P.ty1 - P.ty0 + kTaaH - 1) / kTaaH);
-    if (P.input_half) hipLaunchKernelGGL((k_fused_taa<_Float16>), grd, dim3(256), 0, st, P, taa_args(A));
-    else hipLaunchKernelGGL((k_fused_taa<float>), grd, dim3(256), 0, st, P, taa_args(A));
+    if (P.input_half) hipLaunchKernelGGL((k_fused_taa<_Float16>), grd, dim3(kTaaNT), 0, st, P, taa_args(A));
+    else hipLaunchKernelGGL((k_fused_taa<float>), grd, dim3(kTaaNT), 0, st, P, taa_args(A));
     return hipGetLastError();
 }
 
