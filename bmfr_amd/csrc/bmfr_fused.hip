@@ -138,7 +138,10 @@ __device__ __forceinline__ void block_reduce(float (&v)[K], K1Lds<B>& L, int t) 
 // ---------------------------------------------------------------------------
 // One Householder column (bmfr.cl:549-655), compile-time column index.
 // ---------------------------------------------------------------------------
-template <int col, int B, class M>
+// FAST: bmfr_config.fast_fit -- the trailing update of steps >= 1 as one
+// fused multiply-add on the block-wide factor RN(2 dot / |u|^2) (as
+// update_column in bmfr_fused_cols.hip; not bit-exact).
+template <int col, int B, bool FAST, class M>
 __device__ __forceinline__ void qr_column(M& A, K1Lds<B>& L, int t, const float* __restrict__ noise,
                                           double noise2) {
     constexpr int RE = B - 2;
@@ -244,17 +247,24 @@ __device__ __forceinline__ void qr_column(M& A, K1Lds<B>& L, int t, const float*
         for (int k = 0; k < K; ++k) {
             const int fb = cl + 1 + k;
             const float c2 = 2.f * dot[k];  // 2*u*dot == u*(2*dot): both exact doublings
+            if constexpr (FAST) {
+                const float sc = c2 * recip;
 #pragma unroll
-            for (int s = 0; s < kSubs; ++s)
-                if (s > 0 || t >= cl) A.set(fb, s, A.get(fb, s) - div_by_recip(u[s] * c2, ulen2, recip));
+                for (int s = 0; s < kSubs; ++s)
+                    if (s > 0 || t >= cl) A.set(fb, s, __builtin_fmaf(-u[s], sc, A.get(fb, s)));
+            } else {
+#pragma unroll
+                for (int s = 0; s < kSubs; ++s)
+                    if (s > 0 || t >= cl) A.set(fb, s, A.get(fb, s) - div_by_recip(u[s] * c2, ulen2, recip));
+            }
         }
     }
 }
 
-template <int B, class M, int... C>
+template <int B, bool FAST, class M, int... C>
 __device__ __forceinline__ void qr_columns(M& A, K1Lds<B>& L, int t, const float* __restrict__ noise,
                                            double noise2, std::integer_sequence<int, C...>) {
-    (qr_column<C, B>(A, L, t, noise, noise2), ...);
+    (qr_column<C, B, FAST>(A, L, t, noise, noise2), ...);
 }
 
 // Back substitution (bmfr.cl:658-699) on R in LDS, parallel over elements
@@ -292,7 +302,7 @@ __device__ __forceinline__ void back_substitute(K1Lds<B>& L, int t) {
 // accumulated colour and reprojected positions they read are stored
 // device-coherent and the block publishes done[...] = epoch once they are
 // (the hand-off of bmfr_taa_tile.h wait_k1_blocks).
-template <int NS, int FS, class IN, bool COH = false>
+template <int NS, int FS, class IN, bool COH = false, bool FAST = false>
 __device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K1Lds<NS + FS + 3>& L, int g) {
     constexpr int B = NS + FS + 3;
     const int t = threadIdx.x;
@@ -385,7 +395,7 @@ __device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K
 
     BMFR_STAMP(2);
     // ---- Householder QR over the feature columns (bmfr.cl:544-656) ----
-    qr_columns<B>(M, L, t, A.noise, P.noise2, std::make_integer_sequence<int, B - 3>{});
+    qr_columns<B, FAST>(M, L, t, A.noise, P.noise2, std::make_integer_sequence<int, B - 3>{});
     // Right-hand side: rows 0..B-4 of the colour columns, which the colour
     // columns' own Householder steps never touch (bmfr.cl:550, 596-600, 606).
     if (t < B - 3) {
@@ -460,23 +470,23 @@ __device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K
     }
 }
 
-template <int NS, int FS, class IN>
+template <int NS, int FS, class IN, bool FAST = false>
 __global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
     __shared__ K1Lds<NS + FS + 3> L;
-    k1_rows_body<NS, FS, IN>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
+    k1_rows_body<NS, FS, IN, false, FAST>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
 }
 
 // The one-launch frame with this K1 (f32 tmp_data): K1 blocks, then the
 // frame's TAA tiles waiting on their completion flags (as k_fused_cols_taa,
 // bmfr_fused_cols.hip).
-template <int NS, int FS, class IN>
+template <int NS, int FS, class IN, bool FAST = false>
 __global__ __launch_bounds__(kThreads) void k_fused_rows_taa(Params P, K1Args A, TaaArgs T, int nk1, int nk1p) {
     __shared__ union {
         K1Lds<NS + FS + 3> k1;
         FrameTaaLds<kThreads> k2;
     } U;
     const int b = blockIdx.x;
-    if (b < nk1) k1_rows_body<NS, FS, IN, true>(P, A, U.k1, xcd_swizzle(b, nk1));
+    if (b < nk1) k1_rows_body<NS, FS, IN, true, FAST>(P, A, U.k1, xcd_swizzle(b, nk1));
     else if (b >= nk1p) frame_taa_part<IN, true, kThreads>(P, T, b, nk1p, U.k2);
 }
 
@@ -487,27 +497,42 @@ bool fused_supported(const Params& P) {
     return true;
 }
 
-template <int FS, class IN>
-static void launch_k1(const Params& P, hipStream_t st, const FusedArgs& A) {
-    hipLaunchKernelGGL((k_fused<4, FS, IN>), dim3(k1_blocks(P)), dim3(kThreads), 0, st, P, k1_args(A));
+// The row-split kernels' template arguments from the run-time parameters
+// (FS, the input element type, fast_fit), as dispatch_cols in bmfr_fused_cols.hip.
+template <template <int, class, bool> class L, class... Args>
+static void dispatch_rows(const Params& Q, Args&&... args) {
+    if (Q.scaled == 6) {
+        if (Q.input_half) Q.fast_fit ? L<6, _Float16, true>::go(args...) : L<6, _Float16, false>::go(args...);
+        else Q.fast_fit ? L<6, float, true>::go(args...) : L<6, float, false>::go(args...);
+    } else {
+        if (Q.input_half) Q.fast_fit ? L<9, _Float16, true>::go(args...) : L<9, _Float16, false>::go(args...);
+        else Q.fast_fit ? L<9, float, true>::go(args...) : L<9, float, false>::go(args...);
+    }
 }
 
-template <int FS, class IN>
-static void launch_rows_frame(const Params& P, hipStream_t st, const FusedArgs& A) {
-    const int nk1 = P.ring < 0 || P.nbx <= 0 || P.nby <= 0 ? 0 : k1_blocks(P), nk1p = (nk1 + 7) & ~7;
-    hipLaunchKernelGGL((k_fused_rows_taa<4, FS, IN>), dim3(nk1p + frame_taa_tiles<kThreads>(P)), dim3(kThreads), 0,
-                       st, P, k1_args(A), taa_args(A), nk1, nk1p);
-}
+template <int FS, class IN, bool FAST>
+struct LaunchK1 {
+    static void go(const Params& P, hipStream_t st, const FusedArgs& A) {
+        hipLaunchKernelGGL((k_fused<4, FS, IN, FAST>), dim3(k1_blocks(P)), dim3(kThreads), 0, st, P, k1_args(A));
+    }
+};
+
+template <int FS, class IN, bool FAST>
+struct LaunchRowsFrame {
+    static void go(const Params& P, hipStream_t st, const FusedArgs& A) {
+        const int nk1 = P.ring < 0 || P.nbx <= 0 || P.nby <= 0 ? 0 : k1_blocks(P), nk1p = (nk1 + 7) & ~7;
+        hipLaunchKernelGGL((k_fused_rows_taa<4, FS, IN, FAST>), dim3(nk1p + frame_taa_tiles<kThreads>(P)),
+                           dim3(kThreads), 0, st, P, k1_args(A), taa_args(A), nk1, nk1p);
+    }
+};
 
 hipError_t launch_fused_rows_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
-    if (P.scaled == 6) P.input_half ? launch_rows_frame<6, _Float16>(P, st, A) : launch_rows_frame<6, float>(P, st, A);
-    else P.input_half ? launch_rows_frame<9, _Float16>(P, st, A) : launch_rows_frame<9, float>(P, st, A);
+    dispatch_rows<LaunchRowsFrame>(P, P, st, A);
     return hipGetLastError();
 }
 
 hipError_t launch_fused_k1(const Params& P, hipStream_t st, const FusedArgs& A) {
-    if (P.scaled == 6) P.input_half ? launch_k1<6, _Float16>(P, st, A) : launch_k1<6, float>(P, st, A);
-    else P.input_half ? launch_k1<9, _Float16>(P, st, A) : launch_k1<9, float>(P, st, A);
+    dispatch_rows<LaunchK1>(P, P, st, A);
     return hipGetLastError();
 }
 

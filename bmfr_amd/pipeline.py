@@ -53,7 +53,7 @@ class BmfrConfig:
     # library's powr (== the reference kernel on gfx950) (include/bmfr.h: library_powr)
     library_powr: int = 0
     # Householder trailing update as one fused FMA (not bit-exact, within 3e-6 rel-L2 of the
-    # reference's strict build; column-split K1 only) (include/bmfr.h: fast_fit)
+    # reference's strict build; fused K1, canonical feature lists) (include/bmfr.h: fast_fit)
     fast_fit: int = 0
 
     @property

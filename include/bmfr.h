@@ -124,8 +124,9 @@ typedef struct bmfr_config {
      * factor 2 dot / |u|^2, no longer bit-exact: TAA output within 3e-6
      * relative L2 of the reference's strict build and 1.3e-5 of its default
      * build at 3840x2160 (the two reference builds differ by ~1.2e-5), ~9 %
-     * less K1 time.  Applies to the column-split K1 (canonical feature lists,
-     * half tmp_data, every frame API); other paths run the exact update. */
+     * less K1 time.  Applies to the fused K1 (canonical feature lists, half
+     * or f32 tmp_data, every frame API); the stage fitter (bmfr_fitter) and
+     * the arbitrary-feature-list K1 run the exact update. */
     int fast_fit;
 } bmfr_config;
 

@@ -3,8 +3,9 @@ as one fused multiply-add per element on the block-wide factor
 2 dot / |u|^2 instead of upstream's three roundings -- no longer bit-exact,
 so it is held to north_star's floating-point bar instead: the frame output
 within 1e-4 relative L2 of the reference kernels (oracle/_ref, strict and
-default builds) on the same inputs, at the BASELINE sizes over all 16
-block-grid offsets and over a whole 60-frame sequence (the error does not
+default builds) on the same inputs, at the BASELINE sizes (half and f32
+tmp_data, B = 13 and 16) over all 16 block-grid offsets and over a whole
+60-frame sequence (the error does not
 build up through the temporal accumulation).  The fused update changes only
 the fit's arithmetic, so everything else is checked bit for bit as for the
 exact path: the frame APIs (per-frame one launch, profiled two launches,
@@ -67,7 +68,10 @@ def run_frames(cfg, frames, profiled=False):
 
 
 @pytest.mark.parametrize("W,H,n,kw", [(200, 136, 20, {}), (1920, 1080, 6, {}),
-                                      (256, 144, 6, {"scaled": bmfr_amd.SCALED_THIRD_ORDER})])
+                                      (256, 144, 6, {"scaled": bmfr_amd.SCALED_THIRD_ORDER}),
+                                      (200, 136, 8, {"use_half_precision_in_tmp_data": 0}),
+                                      (256, 144, 6, {"use_half_precision_in_tmp_data": 0,
+                                                     "scaled": bmfr_amd.SCALED_THIRD_ORDER})])
 def test_fast_fit_frame_apis_agree(W, H, n, kw, gpu):
     """One-launch frames == profiled two-launch frames == one
     bmfr_process_sequence call, bit for bit, and the fast fit really differs
@@ -89,7 +93,8 @@ def test_fast_fit_frame_apis_agree(W, H, n, kw, gpu):
 
 
 # (reference build, frames): every block-grid offset at 1080p / 4K, B = 16, a 60-frame sequence
-CASES = [("f1920x1080_h13", 17), ("f3840x2160_h13", 17), ("f3840x2160_h16", 17), ("f1280x720_h13", 60)]
+CASES = [("f1920x1080_h13", 17), ("f3840x2160_h13", 17), ("f3840x2160_h16", 17), ("f3840x2160_f13", 17),
+         ("f1280x720_h13", 60)]
 
 
 @pytest.mark.parametrize("name,n", CASES)
@@ -98,7 +103,8 @@ def test_fast_fit_within_tolerance_of_reference(name, n, gpu, parity_log):
     if not ref_run.available(rc.name):
         pytest.fail(f"reference build {rc.name} missing (oracle/build_ref.py)")
     W, H = rc.width, rc.height
-    cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, scaled=rc.scaled, library_powr=1, fast_fit=1)
+    cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, scaled=rc.scaled, library_powr=1, fast_fit=1,
+                              use_half_precision_in_tmp_data=rc.half_tmp)
     den = bmfr_amd.Denoiser(cfg)
     refs = {m: ref_run.RefLoop(rc, m) for m in ("strict", "default") if ref_run.available(rc.name, m)}
     worst = {m: 0.0 for m in refs}
