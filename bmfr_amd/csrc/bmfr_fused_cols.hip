@@ -36,7 +36,6 @@ namespace cols {
 
 // Waves per work-group NW = 4 (the default) or 8: 64 NW threads; in phase 1
 // and 3 a thread owns kItems = 16 / NW rows of the block.
-constexpr int kThreads = 256;  // NW = 4
 template <int NW>
 constexpr int threads_of() { return 64 * NW; }
 template <int NW>
@@ -580,7 +579,6 @@ __device__ __forceinline__ void back_substitute_regs(Lds<B, NW>& L, int t) {
     }
 }
 
-constexpr int kColsWaves = 4;  // minimum waves per SIMD for the register allocator (128 VGPRs: 4 WGs/CU)
 
 // One K1 work-group (block g of the launch), on the LDS area L.
 // COH: the TAA tiles of the same frame run in this launch: the accumulated
