@@ -88,6 +88,9 @@ def test_default_config_is_reference_defines():
     assert np.float32(c.second_blend_alpha) == np.float32(0.1)
     assert np.float32(c.taa_blend_alpha) == np.float32(0.2)
     assert c.use_half_precision_in_tmp_data == 1
+    # the options beyond the reference's defines default to its behaviour:
+    # untiled, f32 inputs, exact fit (library_powr 0 = the correctly rounded powr)
+    assert (c.tile_width, c.tile_height, c.input_half, c.library_powr, c.fast_fit) == (0, 0, 0, 0, 0)
 
 
 def test_status_strings():
