@@ -129,6 +129,39 @@ def test_fast_fit_within_tolerance_of_reference(name, n, gpu, parity_log):
     print(f"{name}: fast_fit worst output rel-L2 {worst}")
 
 
+def test_bench_configuration_within_tolerance_of_reference(gpu, parity_log):
+    """The exact configuration bench.py's headline times -- 3840x2160, B = 13,
+    half tmp_data, fast_fit, the correctly rounded powr (library_powr = 0) --
+    per frame against the reference's strict build, 17 frames (every
+    block-grid offset): output within 1e-4 relative L2 (the powr's last-bit
+    differences add ~1e-7 to the fit's ~3e-6), temporal state the fit does
+    not feed bit for bit."""
+    rc = FULL_REF_CONFIGS["f3840x2160_h13"]
+    if not ref_run.available(rc.name):
+        pytest.fail(f"reference build {rc.name} missing (oracle/build_ref.py)")
+    W, H = rc.width, rc.height
+    den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H, fast_fit=1))
+    ref = ref_run.RefLoop(rc, "strict")
+    worst = 0.0
+    for f in range(rc.frames):
+        fr = bmfr_amd.synth_frame_device(W, H, f)
+        vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+        _, jit = bmfr_amd.synth_camera(W, H, f)
+        den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, f)
+        got = state(den, W * H)
+        rec = {}
+        ref.upload(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"])
+        ref.run_stages(vp, jit, f, record=rec)
+        ref.swap()
+        e = rel_l2(got["result"], rec["result"])
+        worst = max(worst, e)
+        assert e <= TOL, (f, e)
+        for k in ("noisy", "spp", "prev_pixel"):
+            assert same_bits(got[k], rec[k]), (f, k)
+    parity_log("fast_fit_bench_configuration_f3840x2160_h13", {"frames": rc.frames, "worst_rel_l2_vs_strict": worst})
+    print(f"bench configuration: worst output rel-L2 vs the strict reference {worst:.3g}")
+
+
 def test_fast_fit_tiled_matches_untiled(gpu):
     """The fit is per block: a 2x2 tiling with fast_fit equals the untiled
     fast_fit frames bit for bit (halo exchanged by the loopback transport,
