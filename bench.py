@@ -369,7 +369,7 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     return res
 
 
-def valu_roofline():
+def valu_roofline(fast_fit: bool = False):
     """K1's other roof: VALU issue.  From the committed rocprofv3 SQ pass of
     the same bench command (profiles/*sq_counters.json, newest round):
     K1's VALU instructions per SIMD x the achievable issue cost of a wave64
@@ -380,6 +380,8 @@ def valu_roofline():
     (DESIGN.md section 5)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_sq_counters.json")))
+    if fast_fit:  # the SQ passes of the fast_fit K1, when there are any
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_sq_counters_fastfit.json"))) or files
     if not files:
         return {}
     with open(files[-1]) as f:
@@ -541,7 +543,7 @@ def main():
                    "kernel": "k_fused_cols (K1)" if a.half_tmp else "k_fused (K1)",
                    "algorithmic_bytes_per_launch": k1_bytes_per_px(s) * tile_px}
         if world == 1:
-            k1_roof.update(valu_roofline())
+            k1_roof.update(valu_roofline(a.fast_fit))
         # Untiled per-frame runs with half tmp_data: the frame is one launch
         # (K1 blocks + TAA tiles), the dominant -- only -- kernel of the timed
         # region; its roofline is the frame's algorithmic bytes over its
