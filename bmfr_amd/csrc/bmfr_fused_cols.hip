@@ -137,9 +137,49 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // 4si, 4si+1 of one step feed chains 0, 1 together) run as two packed pairs,
 // and the quotients as packed Markstein steps.  Every lane of a packed op
 // rounds like the scalar op.
+// fast_fit's reach (experiment): 1 = the trailing update only; 2 = also the
+// dot products and pivot norms as fused multiply-add chains.
+#ifndef BMFR_FAST_LEVEL
+#define BMFR_FAST_LEVEL 1
+#endif
+// a_h * b + s in one rounding (the half element widened exactly)
+template <int HI>
+__device__ __forceinline__ float fma_h(h2 h, float b, float s) {
+    float r;
+    if constexpr (HI)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(b), "v"(s));
+    else
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(b), "v"(s));
+    return r;
+}
+
 template <int c, bool FAST = false>
 __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
                                               int l) {
+    if constexpr (FAST && BMFR_FAST_LEVEL >= 2) {
+        // chain m sums rows j = m + 4 si (si = 0..3) as upstream's partials, fused
+        float p[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int si = 0; si < 4; ++si) {
+            const float u0 = si == 0 && l < c ? 0.f : u[4 * si];  // rows above the pivot: skipped
+            p[0] = fma_h<0>(a[2 * si], u0, p[0]);
+            p[1] = fma_h<1>(a[2 * si], u[4 * si + 1], p[1]);
+            p[2] = fma_h<0>(a[2 * si + 1], u[4 * si + 2], p[2]);
+            p[3] = fma_h<1>(a[2 * si + 1], u[4 * si + 3], p[3]);
+        }
+        const float sc = 2.f * wave_reduce<RedOp::Sum>(p) * recip;
+#pragma unroll
+        for (int k = 0; k < kSlots / 2; ++k) {
+            float lo, hi;
+            asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel_hi:[0,0,1]" : "=v"(lo) : "v"(u[2 * k]), "v"(sc), "v"(a[k]));
+            asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+                : "=v"(hi) : "v"(u[2 * k + 1]), "v"(sc), "v"(a[k]));
+            if (k == 0 && l < c) lo = (float)a[0][0];
+            a[k] = __builtin_convertvector((f2v{lo, hi}), h2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        return;
+    }
     f2v s01 = {0.f, 0.f}, s23 = {0.f, 0.f};
 #pragma unroll
     for (int si = 0; si < 4; ++si) {
@@ -295,13 +335,26 @@ __device__ __forceinline__ void wait_all_progress(Lds<B, NW>& L, int c) {
 // The owner of pivot column c (>= 1), once steps 0..c-1 are applied to it:
 // |x|^2 over rows >= c+1, the Householder vector u and |u|^2 (bmfr.cl:555-601),
 // published to LDS with the R column.
-template <int c, int B, int NW>
+template <int c, int B, int NW, bool FAST = false>
 __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B, NW>& L, int l) {
     constexpr int RE = B - 2;
     float x[kSlots];
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
     float p[4];
+    if constexpr (FAST && BMFR_FAST_LEVEL >= 2) {  // fused square-and-add chains
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            float s = 0.f;
+#pragma unroll
+            for (int si = 0; si < 4; ++si) {
+                const int j = m + 4 * si;
+                const float xj = j == 0 && l < c + 1 ? 0.f : x[j];
+                s = __builtin_fmaf(xj, xj, s);
+            }
+            p[m] = s;
+        }
+    } else {
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
         float s = 0.f;
@@ -313,6 +366,7 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B, NW>& L, i
             s = s + pr;
         }
         p[m] = s;
+    }
     }
     const float sumsq = wave_reduce<RedOp::Sum>(p);
     const float ucl = lane_value(x[0], c);  // u_vec[col]: row c is lane c, j = 0
@@ -378,7 +432,7 @@ struct WaveFit {
         if constexpr (c == 0) {
             if (publish) {  // column 1 of wave 0: its first column
                 update_column0(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre[0], NP > 0, noise2);
-                publish_pivot<nxt, B>(a[slot(nxt)], L, l);
+                publish_pivot<nxt, B, NW, FAST>(a[slot(nxt)], L, l);
             }
             sfor<NSL>([&](auto K) {
                 constexpr int k = decltype(K)::value;
@@ -404,7 +458,7 @@ struct WaveFit {
                 if constexpr (nxt < NF) {
                     if (publish) {  // the next pivot is every wave's critical path: issue it first
                         update_column<c, FAST>(a[slot(nxt)], u, ulen2, recip, l);
-                        publish_pivot<nxt, B>(a[slot(nxt)], L, l);
+                        publish_pivot<nxt, B, NW, FAST>(a[slot(nxt)], L, l);
                     }
                 }
                 sfor<NSL>([&](auto K) {

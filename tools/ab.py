@@ -34,7 +34,9 @@ def time_one(W, H, frames=45, first=5):
     import torch
 
     import bmfr_amd
-    den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    # AB_FAST_FIT=1: time the fast_fit configuration
+    den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H,
+                                                fast_fit=int(os.environ.get("AB_FAST_FIT", "0"))))
     fr = [bmfr_amd.synth_frame_device(W, H, f) for f in range(frames)]
     den.set_profiling(True, capacity=frames, stride=1)
     for f in range(frames):
