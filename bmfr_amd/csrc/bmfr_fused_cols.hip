@@ -104,18 +104,8 @@ __device__ __forceinline__ float wave_reduce(const float (&p)[4]) {
     return wave_tree<OP>(step2<OP>(p));
 }
 
-// Mixed-precision FMAs on one half of a packed pair (f16 -> f32 is exact, one
-// rounding): RN(h * b) (fma with -0 addend: exact product, sign of zero kept)
-// and RN(h - q), without separate conversions.
-template <int HI>
-__device__ __forceinline__ float mul_h(h2 h, float b) {
-    float r;
-    if constexpr (HI)
-        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(b), "s"(-0.0f));
-    else
-        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(b), "s"(-0.0f));
-    return r;
-}
+// RN(h - q) on one half of a packed pair (f16 -> f32 is exact, one rounding),
+// without a separate conversion.
 template <int HI>
 __device__ __forceinline__ float sub_h(h2 h, float q) {
     float r;
@@ -132,17 +122,15 @@ __device__ __forceinline__ float sub_h(h2 h, float q) {
 // reciprocal (exact for these operand ranges, tests/test_markstein.py);
 // non-finite or extreme operands take IEEE division (uniform branch).
 typedef float f2v __attribute__((ext_vector_type(2)));
-// Upstream's per-element operations, two rows per instruction: the dot's four
-// partial chains (chain m sums rows j = m + 4 si in order si = 0..3, so rows
-// 4si, 4si+1 of one step feed chains 0, 1 together) run as two packed pairs,
-// and the quotients as packed Markstein steps.  Every lane of a packed op
-// rounds like the scalar op.
-// fast_fit's reach (experiment): 1 = the trailing update only; 2 = also the
-// dot products and pivot norms as fused multiply-add chains.
-#ifndef BMFR_FAST_LEVEL
-#define BMFR_FAST_LEVEL 1
-#endif
-// a_h * b + s in one rounding (the half element widened exactly)
+// Upstream's per-element operations: the dot's four partial chains as fused
+// mixed-precision FMAs (exact products, below), the quotients as packed
+// Markstein steps, two rows per instruction (every lane of a packed op rounds
+// like the scalar op).
+// a_h * b + s in one rounding (the half element widened exactly).  Every
+// product the fit forms this way is exact -- a half times a half (22
+// significant bits) fits a float -- except the pivot row's u element, which
+// only ever enters a chain as its first term (s = 0): so RN(a b + s) equals
+// upstream's RN(RN(a b) + s) bit for bit, in one instruction instead of two.
 template <int HI>
 __device__ __forceinline__ float fma_h(h2 h, float b, float s) {
     float r;
@@ -156,40 +144,18 @@ __device__ __forceinline__ float fma_h(h2 h, float b, float s) {
 template <int c, bool FAST = false>
 __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
                                               int l) {
-    if constexpr (FAST && BMFR_FAST_LEVEL >= 2) {
-        // chain m sums rows j = m + 4 si (si = 0..3) as upstream's partials, fused
-        float p[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int si = 0; si < 4; ++si) {
-            const float u0 = si == 0 && l < c ? 0.f : u[4 * si];  // rows above the pivot: skipped
-            p[0] = fma_h<0>(a[2 * si], u0, p[0]);
-            p[1] = fma_h<1>(a[2 * si], u[4 * si + 1], p[1]);
-            p[2] = fma_h<0>(a[2 * si + 1], u[4 * si + 2], p[2]);
-            p[3] = fma_h<1>(a[2 * si + 1], u[4 * si + 3], p[3]);
-        }
-        const float sc = 2.f * wave_reduce<RedOp::Sum>(p) * recip;
-#pragma unroll
-        for (int k = 0; k < kSlots / 2; ++k) {
-            float lo, hi;
-            asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel_hi:[0,0,1]" : "=v"(lo) : "v"(u[2 * k]), "v"(sc), "v"(a[k]));
-            asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-                : "=v"(hi) : "v"(u[2 * k + 1]), "v"(sc), "v"(a[k]));
-            if (k == 0 && l < c) lo = (float)a[0][0];
-            a[k] = __builtin_convertvector((f2v{lo, hi}), h2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        return;
-    }
-    f2v s01 = {0.f, 0.f}, s23 = {0.f, 0.f};
+    // The dot's four partial chains: chain m sums rows j = m + 4 si in order
+    // si = 0..3 (upstream's work-item partials, bmfr.cl:608-617), fused
+    // (fma_h: exact products, bit for bit upstream's sums).
+    float p[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int si = 0; si < 4; ++si) {
-        f2v p01 = {mul_h<0>(a[2 * si], u[4 * si]), mul_h<1>(a[2 * si], u[4 * si + 1])};
-        const f2v p23 = {mul_h<0>(a[2 * si + 1], u[4 * si + 2]), mul_h<1>(a[2 * si + 1], u[4 * si + 3])};
-        if (si == 0) p01.x = l >= c ? p01.x : 0.f;  // rows above the pivot: skipped
-        s01 = s01 + p01;
-        s23 = s23 + p23;
+        p[0] = fma_h<0>(a[2 * si], u[4 * si], p[0]);
+        if (si == 0) p[0] = l >= c ? p[0] : 0.f;  // rows above the pivot: skipped
+        p[1] = fma_h<1>(a[2 * si], u[4 * si + 1], p[1]);
+        p[2] = fma_h<0>(a[2 * si + 1], u[4 * si + 2], p[2]);
+        p[3] = fma_h<1>(a[2 * si + 1], u[4 * si + 3], p[3]);
     }
-    const float p[4] = {s01.x, s01.y, s23.x, s23.y};
     const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);  // (2u) dot == u (2 dot): same real product, one rounding
     if constexpr (FAST) {
         // bmfr_config.fast_fit (not bit-exact): a - u (2 dot / |u|^2) as one
@@ -341,32 +307,19 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B, NW>& L, i
     float x[kSlots];
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
+    // |x|^2 over rows >= c + 1 (bmfr.cl:555-569): squares of halves are
+    // exact, so the fused square-and-add chains are upstream's sums bit for bit.
     float p[4];
-    if constexpr (FAST && BMFR_FAST_LEVEL >= 2) {  // fused square-and-add chains
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            float s = 0.f;
-#pragma unroll
-            for (int si = 0; si < 4; ++si) {
-                const int j = m + 4 * si;
-                const float xj = j == 0 && l < c + 1 ? 0.f : x[j];
-                s = __builtin_fmaf(xj, xj, s);
-            }
-            p[m] = s;
-        }
-    } else {
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
         float s = 0.f;
 #pragma unroll
         for (int si = 0; si < 4; ++si) {
             const int j = m + 4 * si;
-            float pr = x[j] * x[j];
-            if (j == 0) pr = l >= c + 1 ? pr : 0.f;
-            s = s + pr;
+            const float xj = j == 0 && l < c + 1 ? 0.f : x[j];
+            s = __builtin_fmaf(xj, xj, s);
         }
         p[m] = s;
-    }
     }
     const float sumsq = wave_reduce<RedOp::Sum>(p);
     const float ucl = lane_value(x[0], c);  // u_vec[col]: row c is lane c, j = 0
