@@ -98,10 +98,12 @@ __device__ __forceinline__ float lane_value(float v, int lane) {
 }
 
 // Sum over the wave of upstream work-item partials p[m] (work-item l + 64 m),
-// in upstream's association (bmfr.cl:25-44).
-template <RedOp OP>
+// in upstream's association (bmfr.cl:25-44); with FAST (bmfr_config.fast_fit)
+// a butterfly instead (wave_reduce_fast).
+template <RedOp OP, bool FAST = false>
 __device__ __forceinline__ float wave_reduce(const float (&p)[4]) {
-    return wave_tree<OP>(step2<OP>(p));
+    if constexpr (FAST) return wave_reduce_fast<OP>(p);
+    else return wave_tree<OP>(step2<OP>(p));
 }
 
 // RN(h - q) on one half of a packed pair (f16 -> f32 is exact, one rounding),
@@ -156,13 +158,15 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
         p[2] = fma_h<0>(a[2 * si + 1], u[4 * si + 2], p[2]);
         p[3] = fma_h<1>(a[2 * si + 1], u[4 * si + 3], p[3]);
     }
-    const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);  // (2u) dot == u (2 dot): same real product, one rounding
+    const float c2 = 2.f * wave_reduce<RedOp::Sum, FAST>(p);  // (2u) dot == u (2 dot): same real product, one rounding
     if constexpr (FAST) {
         // bmfr_config.fast_fit (not bit-exact): a - u (2 dot / |u|^2) as one
         // fused mixed-precision FMA per element on the uniform factor
         // RN(c2 / |u|^2), instead of upstream's RN(a - RN(RN(u c2) / |u|^2))
         // -- one rounding (to f32, then half as upstream) where upstream has
-        // three; the dot product stays upstream's.
+        // three.  (fast_fit also sums the wave's partials as a butterfly,
+        // wave_reduce_fast, and takes the pivot's square root, reciprocal
+        // and the feature scaling at hardware precision.)
         const float sc = c2 * recip;
 #pragma unroll
         for (int k = 0; k < kSlots / 2; ++k) {
@@ -221,12 +225,17 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
 // The table holds the float factors (rnd - 0.5f); the term is noise2 * factor
 // in double (bmfr.cl:173-182), formed here: 16 floats per lane -- one round
 // trip for the column's loads.
+template <bool FAST = false>
 __device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const float* __restrict__ noise,
                                                const float (&pre)[kSlots], bool use_pre, double noise2) {
     float x[kSlots];
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
-#define BMFR_ADD_NOISE(xv, r) (float)((double)(xv) + noise2 * (double)(r))
+    // upstream adds the noise in double (one rounding to float); fast_fit:
+    // one f32 FMA on the rounded amount (within an ulp of x)
+    const float noise2f = (float)noise2;
+#define BMFR_ADD_NOISE(xv, r) \
+    (FAST ? __builtin_fmaf(noise2f, (r), (xv)) : (float)((double)(xv) + noise2 * (double)(r)))
     if (use_pre) {  // wave-uniform
 #pragma unroll
         for (int j = 0; j < kSlots; ++j) x[j] = BMFR_ADD_NOISE(x[j], pre[j]);
@@ -249,7 +258,7 @@ __device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const float* _
         }
         p[m] = s;
     }
-    const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);
+    const float c2 = 2.f * wave_reduce<RedOp::Sum, FAST>(p);
     constexpr float ulen2 = 1984.f;
     const float recip = 1.f / ulen2;
     float q, q0;
@@ -321,9 +330,11 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B, NW>& L, i
         }
         p[m] = s;
     }
-    const float sumsq = wave_reduce<RedOp::Sum>(p);
+    const float sumsq = wave_reduce<RedOp::Sum, FAST>(p);
     const float ucl = lane_value(x[0], c);  // u_vec[col]: row c is lane c, j = 0
-    const float vlen = sqrtf(sumsq + ucl * ucl);
+    // fast_fit: the hardware square root and reciprocal (~1 ulp) on the
+    // pivot chain instead of the correctly rounded sequences
+    const float vlen = FAST ? __builtin_amdgcn_sqrtf(sumsq + ucl * ucl) : sqrtf(sumsq + ucl * ucl);
     const float ucl2 = ucl - vlen;
     const float ulen2 = sumsq + ucl2 * ucl2;
     if (l == c) x[0] = ucl2;
@@ -334,7 +345,7 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B, NW>& L, i
     for (int q = 0; q < 4; ++q) dst[q] = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
     if (l == 0) {
         L.piv[buf][0] = ulen2;
-        L.piv[buf][1] = 1.f / ulen2;
+        L.piv[buf][1] = FAST ? __builtin_amdgcn_rcpf(ulen2) : 1.f / ulen2;
     }
     if (l < c) {  // R column: rows above the diagonal, then the diagonal
 #pragma unroll
@@ -384,14 +395,14 @@ struct WaveFit {
         const bool publish = nxt < NF && W == owner(nxt);
         if constexpr (c == 0) {
             if (publish) {  // column 1 of wave 0: its first column
-                update_column0(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre[0], NP > 0, noise2);
+                update_column0<FAST>(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre[0], NP > 0, noise2);
                 publish_pivot<nxt, B, NW, FAST>(a[slot(nxt)], L, l);
             }
             sfor<NSL>([&](auto K) {
                 constexpr int k = decltype(K)::value;
                 const int fb = 1 + W + NW * k;
                 if (owns(W, fb) && !(publish && fb == nxt))  // slots < NP: feature columns, prefetched
-                    update_column0(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr,
+                    update_column0<FAST>(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr,
                                    pre[k < kPre ? k : 0], k < NP, noise2);
             });
         } else {
@@ -496,8 +507,8 @@ struct WaveFit {
                         lo[m] = fminf(v, lo[m]);
                     }
                 }
-                const float bmax = wave_reduce<RedOp::Max>(hi);
-                const float bmin = wave_reduce<RedOp::Min>(lo);
+                const float bmax = wave_reduce<RedOp::Max, FAST>(hi);
+                const float bmin = wave_reduce<RedOp::Min, FAST>(lo);
                 const float d = bmax - bmin;
                 const bool divide = fabsf(d) > 1.0f;  // scale(), bmfr.cl:200-205
                 const float rcp = 1.f / d;
@@ -509,7 +520,9 @@ struct WaveFit {
 #pragma unroll
                 for (int j = 0; j < kSlots; ++j) {
                     const float v = hget(a[k], j) - bmin;
-                    a[k][j >> 1][j & 1] = (_Float16)(divide ? div_by_recip(v, d, rcp) : v);
+                    // fast_fit: one multiply by the rounded reciprocal (as phase 3)
+                    const float sv = FAST ? v * rcp : div_by_recip(v, d, rcp);
+                    a[k][j >> 1][j & 1] = (_Float16)(divide ? sv : v);
                 }
             }
         });
@@ -756,7 +769,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 f2v v = {feature_value(f, nrm[2 * h], wp[2 * h]), feature_value(f, nrm[2 * h + 1], wp[2 * h + 1])};
                 if (f >= NS) {
                     v = v - f2v{bmin, bmin};
-                    if (fabsf(d) > 1.0f) {
+                    if (FAST) {
+                        if (fabsf(d) > 1.0f) v = v * f2v{rcp, rcp};  // fast_fit: as the fit scaled it
+                    } else if (fabsf(d) > 1.0f) {
                         const f2v q0 = v * f2v{rcp, rcp};
                         const f2v r = __builtin_elementwise_fma(-q0, f2v{d, d}, v);
                         v = __builtin_elementwise_fma(r, f2v{rcp, rcp}, q0);

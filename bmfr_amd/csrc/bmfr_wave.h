@@ -100,6 +100,32 @@ __device__ __forceinline__ float step2(const float (&p)[4]) {
     else return red<OP>(red<OP>(red<OP>(p[0], p[1]), p[2]), p[3]);
 }
 
+// bmfr_config.fast_fit: the wave's sum / max / min of the four partials per
+// lane as a butterfly -- quad swaps, half-row and row mirrors by DPP, then the
+// 16- and 32-lane permlane swaps: 6 dependent steps instead of upstream's
+// ~20-step association (wave_tree), so NOT upstream's rounding order.  A sum
+// ends with the same bits in every lane (each level adds two per-group-equal
+// values, a + b == b + a); min / max go through readfirstlane (fmaxf(+0, -0)
+// need not commute).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <RedOp OP>
+__device__ __forceinline__ float wave_reduce_fast(const float (&p)[4]) {
+    float s = red<OP>(red<OP>(p[0], p[1]), red<OP>(p[2], p[3]));
+    s = red<OP>(s, dpp_mov<0xB1>(s));   // quad_perm [1, 0, 3, 2]
+    s = red<OP>(s, dpp_mov<0x4E>(s));   // quad_perm [2, 3, 0, 1]
+    s = red<OP>(s, dpp_mov<0x141>(s));  // row_half_mirror
+    s = red<OP>(s, dpp_mov<0x140>(s));  // row_mirror
+    auto sw = __builtin_amdgcn_permlane16_swap(__float_as_int(s), __float_as_int(s), false, false);
+    s = red<OP>(__int_as_float(sw[0]), __int_as_float(sw[1]));  // rows (0, 1) and (2, 3)
+    sw = __builtin_amdgcn_permlane32_swap(__float_as_int(s), __float_as_int(s), false, false);
+    s = red<OP>(__int_as_float(sw[0]), __int_as_float(sw[1]));  // halves
+    if constexpr (OP != RedOp::Sum) s = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s)));
+    return s;
+}
+
 // K independent sums at once, for one wave: lane l holds the step-2 values
 // v[k] (= s[l] of reduction k).  Steps 64 -> 8 -> 1 (bmfr.cl:35-42) run as an
 // LDS transpose: lane (k, i) forms e_k[i] = s[i] + (((s[i+8] + s[i+16]) + ...)

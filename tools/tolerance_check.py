@@ -4,7 +4,7 @@ reference kernels (oracle/_ref, strict and default builds) frame by frame,
 for builds that are not bit-exact by design (experiments such as
 -DBMFR_FAST_FIT; BMFR_LIB selects the build).  Runs on the GPU box.
 
-  BMFR_LIB=fastfit python tools/tolerance_check.py [CONFIG [FRAMES]]
+  [FAST_FIT=1] BMFR_LIB=NAME python tools/tolerance_check.py [CONFIG [FRAMES]]
   (CONFIG: a FULL_REF_CONFIGS name, default f3840x2160_h13)
 
 The Denoiser runs with library_powr = 1 (the reference kernel's powr), so a
@@ -28,7 +28,7 @@ rc = FULL_REF_CONFIGS[name]
 N = int(sys.argv[2]) if len(sys.argv) > 2 else rc.frames
 W, H = rc.width, rc.height
 cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, scaled=rc.scaled, use_half_precision_in_tmp_data=rc.half_tmp,
-                          library_powr=1)
+                          library_powr=1, fast_fit=int(os.environ.get("FAST_FIT", "0")))
 den = bmfr_amd.Denoiser(cfg)
 refs = {m: ref_run.RefLoop(rc, m) for m in ("strict", "default") if ref_run.available(rc.name, m)}
 out = torch.empty(W * H * 3, device="cuda")
