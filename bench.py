@@ -11,10 +11,11 @@ Workload at N=1: 3840x2160, reference default parameters (B = 13 features,
 half tmp_data, 32x32 blocks), frames W..W+K-1 of the sequence (temporal path
 active on every timed frame), with bmfr_config.fast_fit (--fit fast, the
 default): the fitter's Householder trailing update as one fused FMA per
-element -- within north_star's 1e-4 relative L2 of the reference (measured
-2.5e-6 against its strict build, 1.2e-5 against its default build, which is
-as far from the strict one; tests/test_gpu_fast_fit.py pins exactly this
-configuration at 4K) -- and the exact path (bit-exact to the reference's
+element, its wave-wide reductions as butterflies and its pivot square roots /
+reciprocals at hardware precision -- within north_star's 1e-4 relative L2 of
+the reference (measured 1.2e-5 against its strict build, 1.6e-5 against its
+default build, which is itself 1.2e-5 from the strict one;
+tests/test_gpu_fast_fit.py pins exactly this configuration at 4K) -- and the exact path (bit-exact to the reference's
 strict build, the library's default) as `ms_per_frame_exact` beside it
 (--fit exact swaps the two).
 
@@ -117,7 +118,7 @@ def parse(argv=None):
                          "on gfx950) instead of the correctly rounded one")
     ap.add_argument("--fit", choices=("fast", "exact"), default="fast",
                     help="fast (default): bmfr_config.fast_fit = 1, the fitter's trailing update as one fused FMA "
-                         "(not bit-exact; within 1e-4 -- measured 2.5e-6 -- rel-L2 of the reference's strict build, "
+                         "(not bit-exact; within 1e-4 -- measured 1.2e-5 -- rel-L2 of the reference's strict build, "
                          "tests/test_gpu_fast_fit.py); exact: upstream's roundings, bit-exact to the reference's "
                          "strict build (the library default)")
     ap.add_argument("--no-1080p", action="store_true", help="skip the 1920x1080 line (N = 1 only)")
@@ -582,8 +583,9 @@ def main():
             "config": {"workload": workload, "image": f"{W}x{H}", "buffer_count": cfg.buffer_count,
                        "half_tmp_data": a.half_tmp, "input_half": int(a.input_half),
                        "powr": "device library" if a.library_powr else "correctly rounded",
-                       "fit": ("fast_fit: fused trailing update, within 1e-4 rel-L2 of the reference (measured "
-                               "2.5e-6 vs its strict build, 1.2e-5 vs its default build; tests/test_gpu_fast_fit.py)"
+                       "fit": ("fast_fit: fused trailing update, butterfly reductions, within 1e-4 rel-L2 of the "
+                               "reference (measured 1.2e-5 vs its strict build, 1.6e-5 vs its default build; "
+                               "tests/test_gpu_fast_fit.py)"
                                if a.fast_fit else "exact: bit-exact to the reference's strict build"),
                        "frames_timed": a.steps,
                        "frames_pipelined": world == 1 and a.sequence,

@@ -37,7 +37,7 @@ struct Params {
     int half_tmp;                 // USE_HALF_PRECISION_IN_TMP_DATA
     int input_half;               // bmfr_config.input_half: frame input planes are half3
     int library_powr;             // bmfr_config.library_powr: tone map with __ocml_powr_f32
-    int fast_fit;                 // bmfr_config.fast_fit: fused trailing update in the column-split K1
+    int fast_fit;                 // bmfr_config.fast_fit: fused trailing update (+ butterfly reductions, hardware sqrt / rcp) in the fused K1
     // Buffer region (multi-GPU tiles): every plane of the fused path holds the
     // image pixels [ox, ox + stride) x [oy, oy + rows), row stride `stride`.
     // Untiled: 0, 0, width, height -- the reference's layout.

@@ -121,10 +121,14 @@ typedef struct bmfr_config {
      * element's t - 2 u dot / |u|^2: 0 (default) = upstream's roundings (u * c,
      * then / |u|^2, then the subtraction; the output equals the reference's
      * strict build bit for bit); 1 = one fused multiply-add on the block-wide
-     * factor 2 dot / |u|^2, no longer bit-exact: TAA output within 3e-6
-     * relative L2 of the reference's strict build and 1.3e-5 of its default
-     * build at 3840x2160 (the two reference builds differ by ~1.2e-5), ~9 %
-     * less K1 time.  Applies to the fused K1 (canonical feature lists, half
+     * factor 2 dot / |u|^2, the wave-wide sums, minima and maxima as
+     * butterflies, the noise added in f32 and the pivot's square root,
+     * reciprocals and feature scaling at hardware precision (half tmp_data;
+     * the f32 tmp_data K1 fuses the update only) -- no longer
+     * bit-exact: TAA output within 1.2e-5 relative L2 of the reference's
+     * strict build and 1.6e-5 of its default build at 3840x2160 (3.0e-5 at
+     * B = 16; the two reference builds differ by ~1.2e-5), ~13 % less K1
+     * time.  Applies to the fused K1 (canonical feature lists, half
      * or f32 tmp_data, every frame API); the stage fitter (bmfr_fitter) and
      * the arbitrary-feature-list K1 run the exact update. */
     int fast_fit;
