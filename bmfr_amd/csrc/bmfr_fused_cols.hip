@@ -68,7 +68,7 @@ struct Lds {
     };
     float keep_s[keep_in_m(B) ? 1 : kKeep];
     __device__ float* keep() { return keep_in_m(B) ? keep_m : keep_s; }  // [(item * 3 + ch) * 64 NW + t]
-    float piv[kUBufs][2];               // |u|^2 and RN(1/|u|^2) of the published vector
+    float piv[kUBufs][3];               // |u|^2 and RN(1/|u|^2) of the published vector; fast_fit: u's pivot element
     int pub;                            // highest published pivot column
     int prog[NW];                       // per wave: the last step it has applied
     int timeout;                        // a flag wait of this block gave up (reported once, at the end)
@@ -143,7 +143,35 @@ __device__ __forceinline__ float fma_h(h2 h, float b, float s) {
     return r;
 }
 
-template <int c, bool FAST = false>
+// bmfr_config.fast_fit (not bit-exact): the column update on u as packed
+// halves (publish_pivot: the column's own halves, rows <= c zeroed) plus its
+// pivot element uc (lane c; 0 elsewhere) in f32.  The dot as v_dot2 pairs
+// (half products, f32 sums) and one mixed FMA for the pivot row, summed by
+// the butterfly; a - u (2 dot / |u|^2) as one fused mixed-precision FMA per
+// element on the uniform factor RN(c2 / |u|^2), instead of upstream's
+// RN(a - RN(RN(u c2) / |u|^2)) -- one rounding (to f32, then half as
+// upstream) where upstream has three.  (fast_fit also takes the pivot's
+// square root, reciprocal and the feature scaling at hardware precision.)
+template <int c>
+__device__ __forceinline__ void update_column_fast(h2 (&a)[8], const h2 (&uh)[8], float uc, float recip) {
+    float p[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        p[m] = __builtin_amdgcn_fdot2(a[m + 4], uh[m + 4], __builtin_amdgcn_fdot2(a[m], uh[m], 0.f, false), false);
+    p[0] = fma_h<0>(a[0], uc, p[0]);  // the pivot row (lane c)
+    const float sc = 2.f * wave_reduce_fast<RedOp::Sum>(p) * recip;
+#pragma unroll
+    for (int k = 0; k < kSlots / 2; ++k) {
+        float lo, hi;
+        asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(lo) : "v"(uh[k]), "v"(sc), "v"(a[k]));
+        asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(hi) : "v"(uh[k]), "v"(sc), "v"(a[k]));
+        if (k == 0) lo = __builtin_fmaf(-uc, sc, lo);  // rows above the pivot: u = 0, unchanged
+        a[k] = __builtin_convertvector((f2v{lo, hi}), h2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int c>
 __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
                                               int l) {
     // The dot's four partial chains: chain m sums rows j = m + 4 si in order
@@ -158,28 +186,7 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
         p[2] = fma_h<0>(a[2 * si + 1], u[4 * si + 2], p[2]);
         p[3] = fma_h<1>(a[2 * si + 1], u[4 * si + 3], p[3]);
     }
-    const float c2 = 2.f * wave_reduce<RedOp::Sum, FAST>(p);  // (2u) dot == u (2 dot): same real product, one rounding
-    if constexpr (FAST) {
-        // bmfr_config.fast_fit (not bit-exact): a - u (2 dot / |u|^2) as one
-        // fused mixed-precision FMA per element on the uniform factor
-        // RN(c2 / |u|^2), instead of upstream's RN(a - RN(RN(u c2) / |u|^2))
-        // -- one rounding (to f32, then half as upstream) where upstream has
-        // three.  (fast_fit also sums the wave's partials as a butterfly,
-        // wave_reduce_fast, and takes the pivot's square root, reciprocal
-        // and the feature scaling at hardware precision.)
-        const float sc = c2 * recip;
-#pragma unroll
-        for (int k = 0; k < kSlots / 2; ++k) {
-            float lo, hi;
-            asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel_hi:[0,0,1]" : "=v"(lo) : "v"(u[2 * k]), "v"(sc), "v"(a[k]));
-            asm("v_fma_mix_f32 %0, -%1, %2, %3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-                : "=v"(hi) : "v"(u[2 * k + 1]), "v"(sc), "v"(a[k]));
-            if (k == 0 && l < c) lo = (float)a[0][0];  // rows above the pivot keep their value
-            a[k] = __builtin_convertvector((f2v{lo, hi}), h2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        return;
-    }
+    const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);  // (2u) dot == u (2 dot): same real product, one rounding
     f2v q[kSlots / 2];
     if (fabsf(c2) < 0x1p100f && ulen2 >= 0x1p-100f && ulen2 < 0x1p100f) {
         const f2v vb = {ulen2, ulen2}, vy = {recip, recip};
@@ -340,12 +347,23 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B, NW>& L, i
     if (l == c) x[0] = ucl2;
     constexpr int buf = c % kUBufs;
     if constexpr (c >= kUBufs) wait_all_progress(L, c - kUBufs);  // readers of u_{c-3} done
-    float4* dst = reinterpret_cast<float4*>(&L.u[buf][l * kUStride]);
+    if constexpr (FAST) {  // u as the column's halves, rows <= c zeroed; the pivot element in piv[2]
+        uint32_t w[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dst[q] = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+        for (int k = 0; k < 8; ++k) w[k] = __builtin_bit_cast(uint32_t, a[k]);
+        if (l <= c) w[0] &= 0xffff0000u;
+        uint4* dst = reinterpret_cast<uint4*>(&L.u[buf][l * kUStride]);
+        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    } else {
+        float4* dst = reinterpret_cast<float4*>(&L.u[buf][l * kUStride]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[q] = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+    }
     if (l == 0) {
         L.piv[buf][0] = ulen2;
         L.piv[buf][1] = FAST ? __builtin_amdgcn_rcpf(ulen2) : 1.f / ulen2;
+        L.piv[buf][2] = ucl2;
     }
     if (l < c) {  // R column: rows above the diagonal, then the diagonal
 #pragma unroll
@@ -408,20 +426,35 @@ struct WaveFit {
         } else {
             if (1 + W + NW * ((B - 2 - W) / NW) > c) {  // this wave's last column is past the pivot
                 wait_pub(L, c);
-                float u[kSlots];
-                const float4* src = reinterpret_cast<const float4*>(&L.u[c % kUBufs][l * kUStride]);
+                float u[FAST ? 1 : kSlots];
+                h2 uh[FAST ? 8 : 1];
+                float uc = 0.f;
+                if constexpr (FAST) {
+                    const uint4* src = reinterpret_cast<const uint4*>(&L.u[c % kUBufs][l * kUStride]);
+                    const uint4 v0 = src[0], v1 = src[1];
+                    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 v = src[q];
-                    u[4 * q] = v.x;
-                    u[4 * q + 1] = v.y;
-                    u[4 * q + 2] = v.z;
-                    u[4 * q + 3] = v.w;
+                    for (int k = 0; k < 8; ++k) uh[k] = __builtin_bit_cast(h2, w[k]);
+                    uc = l == c ? L.piv[c % kUBufs][2] : 0.f;
+                } else {
+                    const float4* src = reinterpret_cast<const float4*>(&L.u[c % kUBufs][l * kUStride]);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float4 v = src[q];
+                        u[4 * q] = v.x;
+                        u[4 * q + 1] = v.y;
+                        u[4 * q + 2] = v.z;
+                        u[4 * q + 3] = v.w;
+                    }
                 }
                 const float ulen2 = L.piv[c % kUBufs][0], recip = L.piv[c % kUBufs][1];
+                auto upd = [&](h2 (&col)[8]) {
+                    if constexpr (FAST) update_column_fast<c>(col, uh, uc, recip);
+                    else update_column<c>(col, u, ulen2, recip, l);
+                };
                 if constexpr (nxt < NF) {
                     if (publish) {  // the next pivot is every wave's critical path: issue it first
-                        update_column<c, FAST>(a[slot(nxt)], u, ulen2, recip, l);
+                        upd(a[slot(nxt)]);
                         publish_pivot<nxt, B, NW, FAST>(a[slot(nxt)], L, l);
                     }
                 }
@@ -429,8 +462,7 @@ struct WaveFit {
                     constexpr int k = decltype(K)::value;
                     const int fb = 1 + W + NW * k;
                     if constexpr (NW * k + NW > c) {  // slot k holds columns <= NW k + NW
-                        if (owns(W, fb) && fb > c && !(publish && fb == nxt))
-                            update_column<c, FAST>(a[k], u, ulen2, recip, l);
+                        if (owns(W, fb) && fb > c && !(publish && fb == nxt)) upd(a[k]);
                     }
                 });
             }
