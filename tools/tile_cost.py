@@ -4,7 +4,7 @@ tile of a tx x ty grid of W x H tiles, each frame as process_frame or as
 process_frame_interior + process_frame_border (halo left stale: timing only),
 against the untiled W x H frame.  Prints ms/frame for each.
 
-  python tools/tile_cost.py [W H TX TY RANK]   (default: 3840 2160 4 2 5;
+  [FAST_FIT=1] python tools/tile_cost.py [W H TX TY RANK]   (default: 3840 2160 4 2 5;
   the 8K strong-scaling tile of 8 GPUs: 1920 2160 4 2 5)"""
 import os
 import sys
@@ -43,8 +43,10 @@ def run(cfg, split):
     return 1e3 * (time.perf_counter() - t0) / (FR - 5)
 
 
-full = bmfr_amd.BmfrConfig(image_width=W, image_height=H)
-tile = bmfr_amd.BmfrConfig(image_width=W * TX, image_height=H * TY, tile=grid.tile(RANK), tile_halo=64)
+FAST = int(os.environ.get("FAST_FIT", "0"))  # FAST_FIT=1: bmfr_config.fast_fit (the bench headline's fit)
+full = bmfr_amd.BmfrConfig(image_width=W, image_height=H, fast_fit=FAST)
+tile = bmfr_amd.BmfrConfig(image_width=W * TX, image_height=H * TY, tile=grid.tile(RANK), tile_halo=64, fast_fit=FAST)
+print(f"fast_fit = {FAST}")
 print(f"untiled {W}x{H}: {run(full, False):.4f} ms/frame")
 print(f"tile {grid.tile(RANK)} of {W * TX}x{H * TY}, one call: {run(tile, False):.4f} ms/frame")
 print(f"same tile, interior + border calls: {run(tile, True):.4f} ms/frame")
