@@ -127,7 +127,7 @@ typedef struct bmfr_config {
      * the f32 tmp_data K1 fuses the update only) -- no longer
      * bit-exact: TAA output within 1.2e-5 relative L2 of the reference's
      * strict build and 1.6e-5 of its default build at 3840x2160 (3.0e-5 at
-     * B = 16; the two reference builds differ by ~1.2e-5), ~13 % less K1
+     * B = 16; the two reference builds differ by ~1.2e-5), ~15 % less K1
      * time.  Applies to the fused K1 (canonical feature lists, half
      * or f32 tmp_data, every frame API); the stage fitter (bmfr_fitter) and
      * the arbitrary-feature-list K1 run the exact update. */
