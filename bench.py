@@ -239,7 +239,10 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     # start/end, border end) events, on the streams the work runs on.
     marks = []
 
+    host_issue = []  # tiled frames: host wall time to enqueue one frame (interior, pack, exchange, unpack, border)
+
     def run(f, mark=False):
+        t_issue = time.perf_counter()
         fr = frames[f]
         prev = frames[f - 1] if f > 0 else None
         args = (fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], cams[f][0], cams[f][1], f)
@@ -270,6 +273,8 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
                 marks.append((ev, transport.last_bytes))
         if frame_done is not None:
             frame_done.record(compute)
+            if f > 0:
+                host_issue.append(time.perf_counter() - t_issue)
 
     # Untiled: the whole run as bmfr_process_sequence calls (frames pipelined),
     # unless per_frame; tiled: frame by frame around the halo exchange.
@@ -352,7 +357,10 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
                  "frame_ms": mean(0, 4),
                  "halo_bytes_sent": int(np.mean([b[0] for _, b in marks])),
                  "halo_bytes_received": int(np.mean([b[1] for _, b in marks])),
-                 "halo_overshoot_px": overshoot}
+                 "halo_overshoot_px": overshoot,
+                 # host time to enqueue one tiled frame (mean over timed frames > 0);
+                 # with gloo this includes the blocking host-staged transfer
+                 "host_issue_ms": 1e3 * float(np.mean(host_issue[-steps:])) if host_issue else 0.0}
     res = {
         "cfg": cfg,
         "ms_per_frame": 1e3 * elapsed / steps,
@@ -523,7 +531,8 @@ def main():
                                          per_frame=True))
     ranks = None
     if world > 1 and r["split"] is not None:
-        keys = ("interior_ms", "exchange_ms", "border_ms", "frame_ms", "halo_bytes_sent", "halo_overshoot_px")
+        keys = ("interior_ms", "exchange_ms", "border_ms", "frame_ms", "host_issue_ms", "halo_bytes_sent",
+                "halo_overshoot_px")
         v = torch.zeros(world, len(keys), dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         v[rank] = torch.tensor([float(r["split"][k]) for k in keys], dtype=torch.float64)
         dist.all_reduce(v)
@@ -588,6 +597,9 @@ def main():
                                "tests/test_gpu_fast_fit.py)"
                                if a.fast_fit else "exact: bit-exact to the reference's strict build"),
                        "frames_timed": a.steps,
+                       # SHA-256 of the sources libbmfr.so was built from (the loader
+                       # refuses a library that is not this tree's: bmfr_amd/_lib.py)
+                       "build_id": bmfr_amd.build_id(),
                        "frames_pipelined": world == 1 and a.sequence,
                        "parallelism": (f"tiles {tx}x{ty}, halo {a.halo} px, "
                                        f"{'RCCL' if backend == 'nccl' else backend} halo exchange"

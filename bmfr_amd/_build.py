@@ -7,6 +7,7 @@ per-operation rounding (see csrc/bmfr_device.h).
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 
@@ -21,10 +22,47 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=o
          "-Wall", "-Wno-unused-function"]
 
 
-def _deps_mtime() -> float:
-    files = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
-    files.append(os.path.join(HERE, "..", "include", "bmfr.h"))
-    return max(os.path.getmtime(f) for f in files)
+INCLUDE = os.path.join(HERE, "..", "include")
+ID_MARK = b"bmfr-build-id:"
+
+
+def source_files() -> list:
+    """Every file libbmfr.so is compiled from: csrc/ and the public headers."""
+    files = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith((".hip", ".h"))]
+    files += [os.path.join(INCLUDE, f) for f in sorted(os.listdir(INCLUDE)) if f.endswith(".h")]
+    return files
+
+
+def source_hash() -> str:
+    """SHA-256 over the library's sources (names and contents): the build id
+    libbmfr.so carries (bmfr_build_id()) and the loader checks (_lib.load)."""
+    h = hashlib.sha256()
+    for f in source_files():
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def build_id(diag: bool = False, extra_flags=()) -> str:
+    """The id a build of the current sources with these options carries:
+    the source hash, then '+' and the extra compile flags of a variant."""
+    flags = (["-DBMFR_STAMPS"] if diag else []) + [f for f in extra_flags if f]
+    return source_hash() + ("+" + ",".join(flags) if flags else "")
+
+
+def embedded_id(lib: str) -> str | None:
+    """The build id stored in a built library (read from the file: no dlopen)."""
+    if not os.path.exists(lib):
+        return None
+    with open(lib, "rb") as f:
+        data = f.read()
+    i = data.find(ID_MARK)
+    if i < 0:
+        return None
+    j = data.index(b"\0", i)
+    return data[i + len(ID_MARK):j].decode()
 
 
 class _BuildLock:
@@ -65,14 +103,18 @@ def _build(force, verbose, diag, variant, extra_flags) -> str:
     variant=NAME, libbmfr_NAME.so built with extra_flags, for A/B timing --
     selected at run time by BMFR_LIB=NAME)."""
     lib = DIAG_LIB if diag else (os.path.join(HERE, f"libbmfr_{variant}.so") if variant else LIB)
-    if not force and os.path.exists(lib) and os.path.getmtime(lib) >= _deps_mtime():
+    want = build_id(diag, extra_flags)
+    if not force and embedded_id(lib) == want:
         return lib
     objdir = os.path.join(HERE, "_obj_diag" if diag else (f"_obj_{variant}" if variant else "_obj"))
     os.makedirs(objdir, exist_ok=True)
+    # the id, as a generated header only bmfr_capi.hip includes (bmfr_build_id())
+    with open(os.path.join(objdir, "bmfr_build_id.h"), "w") as f:
+        f.write(f'#define BMFR_BUILD_ID "{want}"\n')
 
     def compile_one(src: str) -> str:
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
-        cmd = [HIPCC, *FLAGS, *(["-DBMFR_STAMPS"] if diag else []), *extra_flags, "-c",
+        cmd = [HIPCC, *FLAGS, *(["-DBMFR_STAMPS"] if diag else []), *extra_flags, "-I", objdir, "-c",
                os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
@@ -85,6 +127,22 @@ def _build(force, verbose, diag, variant, extra_flags) -> str:
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs], check=True)
     os.replace(tmp, lib)
     return lib
+
+
+TOOLS = os.path.join(HERE, "..", "tools")
+
+
+def build_tool(src: str, out: str) -> str:
+    """A stand-alone HIP experiment library under tools/ (e.g. libwy.so), with
+    the same build lock and the same never-rebuild-on-the-GPU-box rule."""
+    src, out = os.path.join(TOOLS, src), os.path.join(TOOLS, out)
+    if os.path.exists(out) and (_on_gpu_box() or os.path.getmtime(out) >= os.path.getmtime(src)):
+        return out
+    with _BuildLock():
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", src, "-o",
+                        out + ".tmp"], check=True)
+        os.replace(out + ".tmp", out)
+    return out
 
 
 HOST_DIR = os.path.join(HERE, "..", "host")

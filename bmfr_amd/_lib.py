@@ -94,6 +94,7 @@ SIGNATURES = {
     "bmfr_config_sizes": (_I, [C.POINTER(Config), C.POINTER(Sizes)]),
     "bmfr_status_string": (C.c_char_p, [_I]),
     "bmfr_last_hip_error": (_I, []),
+    "bmfr_build_id": (C.c_char_p, []),
     "bmfr_create": (_I, [C.POINTER(Config), _I, C.POINTER(_P)]),
     "bmfr_destroy": (_I, [_P]),
     "bmfr_get_sizes": (_I, [_P, C.POINTER(Sizes)]),
@@ -127,13 +128,44 @@ SIGNATURES = {
 _lib = None
 
 
+class StaleLibraryError(ImportError):
+    """The library on disk was not built from the sources in this tree."""
+
+
+def check_build_id(lib: C.CDLL, path: str) -> str:
+    """Refuse a library built from other sources than this tree's (the id is
+    the SHA-256 of csrc/ + include/, _build.source_hash) or a probe build
+    (BMFR_PROBE_* flags: timing experiments with knowingly wrong results)
+    unless BMFR_ALLOW_PROBE=1.  Never rebuilds: on the GPU box the library
+    that runs must be the one shipped with the tree."""
+    from . import _build
+    if not hasattr(lib, "bmfr_build_id"):
+        raise StaleLibraryError(f"{path} predates bmfr_build_id(): rebuild it (__graft_entry__.build())")
+    lib.bmfr_build_id.restype = C.c_char_p
+    got = lib.bmfr_build_id().decode()
+    want = _build.source_hash()
+    if got.split("+")[0] != want:
+        raise StaleLibraryError(f"{path} was built from other sources (build id {got[:16]}..., tree "
+                                f"{want[:16]}...): rebuild it (__graft_entry__.build())")
+    if "BMFR_PROBE" in got and os.environ.get("BMFR_ALLOW_PROBE") != "1":
+        raise StaleLibraryError(f"{path} is a probe build ({got.split('+', 1)[1]}): its results are not "
+                                f"guaranteed; set BMFR_ALLOW_PROBE=1 to time it anyway")
+    return got
+
+
+def build_id() -> str:
+    return load().bmfr_build_id().decode()
+
+
 def load() -> C.CDLL:
-    """Load libbmfr.so; raises if it has not been built (no silent fallback)."""
+    """Load libbmfr.so; raises if it has not been built, or was built from
+    other sources (no silent fallback, no rebuild)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
         lib = C.CDLL(LIB_PATH)
+        check_build_id(lib, LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             if _variant and not hasattr(lib, name):
                 continue  # an A/B build of older sources may predate a symbol

@@ -322,6 +322,17 @@ const char* bmfr_status_string(bmfr_status s) {
 
 int bmfr_last_hip_error(void) { return g_last_hip_error; }
 
+// The build id (bmfr_amd/_build.py: SHA-256 of the sources, then "+flags" for
+// a variant build), behind a marker so the build script can read it from the
+// file without loading it.
+#if __has_include("bmfr_build_id.h")
+#include "bmfr_build_id.h"
+#else
+#define BMFR_BUILD_ID "unknown"
+#endif
+static const char kBuildId[] = "bmfr-build-id:" BMFR_BUILD_ID;
+const char* bmfr_build_id(void) { return kBuildId + sizeof("bmfr-build-id:") - 1; }
+
 bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
     if (!out) return BMFR_ERROR_INVALID_ARGUMENT;
     *out = nullptr;

@@ -107,7 +107,10 @@ __device__ __forceinline__ float wave_reduce(const float (&p)[4]) {
 }
 
 // RN(h - q) on one half of a packed pair (f16 -> f32 is exact, one rounding),
-// without a separate conversion.
+// without a separate conversion.  Inline asm (the compiler makes a conversion
+// plus a subtraction of fmaf(h, 1, -q)): its operands never come from a DOT or
+// transcendental instruction, the producers whose wait states the compiler
+// cannot insert for an asm reader -- tools/isa_hazards.py checks the built code.
 template <int HI>
 __device__ __forceinline__ float sub_h(h2 h, float q) {
     float r;
@@ -133,14 +136,16 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // significant bits) fits a float -- except the pivot row's u element, which
 // only ever enters a chain as its first term (s = 0): so RN(a b + s) equals
 // upstream's RN(RN(a b) + s) bit for bit, in one instruction instead of two.
+// Written as fmaf on the widened half, which the compiler selects as one
+// v_fma_mix_f32 -- NOT as inline asm: gfx950 needs three wait states between
+// a DOT instruction writing a VGPR and another VALU instruction reading it
+// (fast_fit feeds v_dot2 sums into this FMA), and the compiler's hazard
+// recognizer inserts them only for instructions it can see.  As inline asm
+// this was the round-3 "ordering bug" that a sched_barrier happened to hide
+// (tools/isa_hazards.py, tests/test_isa_hazards.py).
 template <int HI>
 __device__ __forceinline__ float fma_h(h2 h, float b, float s) {
-    float r;
-    if constexpr (HI)
-        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(b), "v"(s));
-    else
-        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(b), "v"(s));
-    return r;
+    return __builtin_fmaf((float)h[HI], b, s);
 }
 
 // bmfr_config.fast_fit (not bit-exact): the column update on u as packed
@@ -152,6 +157,16 @@ __device__ __forceinline__ float fma_h(h2 h, float b, float s) {
 // RN(a - RN(RN(u c2) / |u|^2)) -- one rounding (to f32, then half as
 // upstream) where upstream has three.  (fast_fit also takes the pivot's
 // square root, reciprocal and the feature scaling at hardware precision.)
+// The update's FMAs are inline asm (the compiler would widen both halves
+// first); their operands are u (LDS), the column (a conversion) and sc (a
+// multiply) -- never a DOT result, so no hidden wait state is owed.  The pivot
+// row's FMA, which reads the v_dot2 chain, is fma_h (compiler-visible).
+// The scheduling barrier at the end is a register-footprint knob only
+// (-DBMFR_FAST_SCHED_BARRIER=0 builds without it; tests/test_gpu_fast_fit.py
+// runs that build against the exact path).
+#ifndef BMFR_FAST_SCHED_BARRIER
+#define BMFR_FAST_SCHED_BARRIER 1
+#endif
 template <int c>
 __device__ __forceinline__ void update_column_fast(h2 (&a)[8], const h2 (&uh)[8], float uc, float recip) {
     float p[4];
@@ -168,7 +183,9 @@ __device__ __forceinline__ void update_column_fast(h2 (&a)[8], const h2 (&uh)[8]
         if (k == 0) lo = __builtin_fmaf(-uc, sc, lo);  // rows above the pivot: u = 0, unchanged
         a[k] = __builtin_convertvector((f2v{lo, hi}), h2);
     }
+#if BMFR_FAST_SCHED_BARRIER
     __builtin_amdgcn_sched_barrier(0);
+#endif
 }
 
 template <int c>

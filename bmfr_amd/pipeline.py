@@ -52,8 +52,10 @@ class BmfrConfig:
     # Tone map powr: 0 = correctly rounded (== the CPU oracle), 1 = the device
     # library's powr (== the reference kernel on gfx950) (include/bmfr.h: library_powr)
     library_powr: int = 0
-    # Householder trailing update as one fused FMA (not bit-exact, within 3e-6 rel-L2 of the
-    # reference's strict build; fused K1, canonical feature lists) (include/bmfr.h: fast_fit)
+    # Householder trailing update as one fused FMA, butterfly reductions, hardware sqrt / rcp on
+    # the pivot chain (not bit-exact: measured <= 1.2e-5 rel-L2 of the reference's strict build
+    # at 4K, 3.0e-5 at B = 16; the tests hold it to north_star's 1e-4; fused K1, canonical
+    # feature lists) (include/bmfr.h: fast_fit)
     fast_fit: int = 0
 
     @property

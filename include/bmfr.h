@@ -157,6 +157,11 @@ void bmfr_config_default(bmfr_config *cfg, int image_width, int image_height);
 bmfr_status bmfr_config_sizes(const bmfr_config *cfg, bmfr_sizes *out);
 const char *bmfr_status_string(bmfr_status s);
 int bmfr_last_hip_error(void);
+/* Identity of the compiled library: SHA-256 (hex) of the sources it was built
+ * from, followed by "+<flags>" for a variant build.  No reference counterpart
+ * (the reference JIT-compiles bmfr.cl at start-up, bmfr.cpp:234-243, so its
+ * binary is always its source); here it ties a shipped binary to its tree. */
+const char *bmfr_build_id(void);
 
 /* Replaces clutils::CLEnv + the addContext/addQueue/addProgram calls
  * (bmfr.cpp:183-243): binds a HIP device and selects the kernels. */

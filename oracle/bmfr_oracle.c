@@ -359,6 +359,25 @@ static float tree_min(const float s_in[LSIZE]) {   /* bmfr.cl:46-66 */
     return r;
 }
 
+/* Experiment hook, off in the oracle (tools/panel_rounding.py builds a
+ * separate library with -DORACLE_PANEL_EXPERIMENT): with a panel width
+ * g_panel > 0, a trailing column beyond the current panel of pivot columns is
+ * rounded to half only at the panel's last step -- the arithmetic of a blocked
+ * (compact-WY) trailing update -- instead of after every step (bmfr.cl:651). */
+#ifdef ORACLE_PANEL_EXPERIMENT
+static int g_panel = 0;
+void oracle_set_panel(int nb) { g_panel = nb; }
+static int panel_rounds(int col, int fb, int B) {
+    if (g_panel <= 0 || col >= B - 3) return 1;  /* g_panel < 0: dots-only mode, below */
+    int end = (col / g_panel + 1) * g_panel;
+    if (end > B - 3) end = B - 3;
+    return fb < end || col == end - 1;
+}
+#define PANEL_ROUNDS(col, fb, B) panel_rounds(col, fb, B)
+#else
+#define PANEL_ROUNDS(col, fb, B) 1
+#endif
+
 /* One fitter work-group (bmfr.cl:490-700) on block g.  The block's design
  * matrix is kept as A[feature][row], row = y*32 + x; work-item t of the
  * reference owns rows t + 256*s, s = 0..3. */
@@ -374,6 +393,9 @@ static void fit_block(const oracle_cfg *c, float *weights, float *mins_maxs, voi
      * before use or never read). */
     float R[ORACLE_MAX_FEATURES + 1][ORACLE_MAX_FEATURES + 1][3];
     memset(R, 0, sizeof(R));
+#ifdef ORACLE_PANEL_EXPERIMENT
+    static _Thread_local float Sh[ORACLE_MAX_FEATURES + 3][PIXELS];
+#endif
 
     for (int f = 0; f < B; ++f)
         for (int r = 0; r < PIXELS; ++r) A[f][r] = tmp_load(c, tmp, base + (size_t)f * PIXELS + r);
@@ -428,8 +450,19 @@ static void fit_block(const oracle_cfg *c, float *weights, float *mins_maxs, voi
             for (int y = 0; y < B - 3; ++y) R[cl][y][ch] = A[col][y];
         }
         /* Transform the trailing columns (bmfr.cl:606-655). */
+#ifdef ORACLE_PANEL_EXPERIMENT
+        /* dots-only mode (g_panel < 0): the trailing columns' dot products from
+         * an unrounded shadow, as V^T X with the WY identity would give them;
+         * the updates still rounded every step */
+        if (g_panel < 0 && col < B - 3 && col % -g_panel == 0)
+            for (int f = 0; f < B; ++f)
+                for (int r = 0; r < PIXELS; ++r) Sh[f][r] = A[f][r];
+#endif
         for (int fb = cl + 1; fb < B; ++fb) {
             float cache[LSIZE][SUBS];
+#ifdef ORACLE_PANEL_EXPERIMENT
+            const int shadow = g_panel < 0 && col < B - 3 && fb >= (col / -g_panel + 1) * -g_panel;
+#endif
             for (int t = 0; t < LSIZE; ++t) {
                 float sum = 0.f;
                 for (int s = 0; s < SUBS; ++s) {
@@ -438,6 +471,14 @@ static void fit_block(const oracle_cfg *c, float *weights, float *mins_maxs, voi
                         float v = A[fb][i];
                         if (col == 0 && fb < B - 3) v = add_random(c, v, t, s, fb, frame);
                         cache[t][s] = v;
+#ifdef ORACLE_PANEL_EXPERIMENT
+                        if (shadow) {
+                            float w = Sh[fb][i];
+                            if (col == 0 && fb < B - 3) w = add_random(c, w, t, s, fb, frame);
+                            sum = sum + w * u[i];
+                            continue;
+                        }
+#endif
                         sum = sum + v * u[i];
                     }
                 }
@@ -449,8 +490,15 @@ static void fit_block(const oracle_cfg *c, float *weights, float *mins_maxs, voi
                     const int i = t + s * LSIZE;
                     if (i >= cl) {
                         float v = cache[t][s];
+#ifdef ORACLE_PANEL_EXPERIMENT
+                        if (shadow) {
+                            float w = Sh[fb][i];
+                            if (col == 0 && fb < B - 3) w = add_random(c, w, t, s, fb, frame);
+                            Sh[fb][i] = w - 2 * u[i] * dot / ulen2;
+                        }
+#endif
                         v = v - 2 * u[i] * dot / ulen2;
-                        A[fb][i] = c->half_tmp ? oracle_f16_to_f32(oracle_f32_to_f16(v)) : v;
+                        A[fb][i] = c->half_tmp && PANEL_ROUNDS(col, fb, B) ? oracle_f16_to_f32(oracle_f32_to_f16(v)) : v;
                     }
                 }
         }

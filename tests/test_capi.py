@@ -158,3 +158,38 @@ def test_split_frame_calls_validate_arguments():
     lib = _lib.load()
     assert lib.bmfr_process_frame_interior(None, None, None, None, None, 0) == 1
     assert lib.bmfr_process_frame_border(None, None, None, None, None, 0) == 1
+
+
+def test_library_build_id_is_the_tree():
+    """libbmfr.so carries the SHA-256 of the sources it was built from, and
+    it is this tree's (the loader refuses anything else)."""
+    from bmfr_amd import _build
+    lib = _lib.load()
+    assert lib.bmfr_build_id().decode() == _build.source_hash()
+    assert _build.embedded_id(_lib.LIB_PATH) == _build.source_hash()
+
+
+def _fake_lib(tmp_path, ident: str, name: str) -> str:
+    import subprocess
+    src = tmp_path / f"{name}.c"
+    src.write_text('const char* bmfr_build_id(void) { return "%s"; }\n' % ident)
+    so = str(tmp_path / f"lib{name}.so")
+    subprocess.run(["gcc", "-shared", "-fPIC", str(src), "-o", so], check=True)
+    return so
+
+
+def test_mismatched_library_is_refused(tmp_path, monkeypatch):
+    from bmfr_amd import _build
+    so = _fake_lib(tmp_path, "0" * 64, "stale")
+    with pytest.raises(_lib.StaleLibraryError, match="other sources"):
+        _lib.check_build_id(C.CDLL(so), so)
+    # a probe build of the right sources is refused too, unless asked for
+    probe = _fake_lib(tmp_path, _build.source_hash() + "+-DBMFR_PROBE_NOSC1", "probe")
+    monkeypatch.delenv("BMFR_ALLOW_PROBE", raising=False)
+    with pytest.raises(_lib.StaleLibraryError, match="probe build"):
+        _lib.check_build_id(C.CDLL(probe), probe)
+    monkeypatch.setenv("BMFR_ALLOW_PROBE", "1")
+    assert _lib.check_build_id(C.CDLL(probe), probe).endswith("BMFR_PROBE_NOSC1")
+    # a variant of the right sources is accepted
+    ok = _fake_lib(tmp_path, _build.source_hash() + "+-DBMFR_FAST_SCHED_BARRIER=0", "variant")
+    assert _lib.check_build_id(C.CDLL(ok), ok)

@@ -166,6 +166,46 @@ def test_bench_configuration_within_tolerance_of_reference(gpu, parity_log):
     print(f"bench configuration: worst output rel-L2 vs the strict reference {worst:.3g}")
 
 
+def test_cfg5_timed_configuration_within_tolerance_of_reference(gpu, parity_log):
+    """BASELINE config 5 exactly as bench.py times it (ms_per_frame_cfg5):
+    3840x2160, half input planes, B = 16 (3rd-order positions), half
+    tmp_data, fast_fit, the correctly rounded powr -- per frame against the
+    reference kernels run on the same planes widened to f32 (what the half
+    path reads), 17 frames (every block-grid offset): output within 1e-4
+    relative L2 of the strict and the default build, the temporal state the
+    fit does not feed bit for bit (strict)."""
+    rc = FULL_REF_CONFIGS["f3840x2160_h16"]
+    if not ref_run.available(rc.name):
+        pytest.fail(f"reference build {rc.name} missing (oracle/build_ref.py)")
+    W, H = rc.width, rc.height
+    den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H, scaled=rc.scaled, fast_fit=1,
+                                                input_half=1))
+    refs = {m: ref_run.RefLoop(rc, m) for m in ("strict", "default") if ref_run.available(rc.name, m)}
+    worst = {m: 0.0 for m in refs}
+    for f in range(rc.frames):
+        fr = bmfr_amd.synth_frame_device(W, H, f, seed=rc.seed)
+        h = {k: fr[k].half() for k in ("noisy", "normals", "positions", "albedo")}
+        w = {k: v.float() for k, v in h.items()}
+        del fr
+        vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+        _, jit = bmfr_amd.synth_camera(W, H, f)
+        den.process_frame(h["noisy"], h["normals"], h["positions"], h["albedo"], vp, jit, f)
+        got = state(den, W * H)
+        for m, rl in refs.items():
+            rec = {}
+            rl.upload(w["noisy"], w["normals"], w["positions"], w["albedo"])
+            rl.run_stages(vp, jit, f, record=rec)
+            rl.swap()
+            e = rel_l2(got["result"], rec["result"])
+            worst[m] = max(worst[m], e)
+            assert e <= TOL, (f, m, e)
+            if m == "strict":
+                for k in ("noisy", "spp", "prev_pixel"):
+                    assert same_bits(got[k], rec[k]), (f, k)
+    parity_log("fast_fit_cfg5_timed_f3840x2160_h16_in16", {"frames": rc.frames, "worst_rel_l2": worst})
+    print(f"config 5 timed configuration: worst output rel-L2 {worst}")
+
+
 def test_fast_fit_tiled_matches_untiled(gpu):
     """The fit is per block: a 2x2 tiling with fast_fit equals the untiled
     fast_fit frames bit for bit (halo exchanged by the loopback transport,
@@ -199,3 +239,38 @@ def test_fast_fit_tiled_matches_untiled(gpu):
             tx, ty, tw, th = grid.tile(r)
             a = got[ty - y0:ty - y0 + th, tx - x0:tx - x0 + tw].contiguous()
             assert same_bits(a, want[ty:ty + th, tx:tx + tw].contiguous()), f"frame {f} tile {r}"
+
+
+def test_fast_fit_without_sched_barrier(gpu, tmp_path):
+    """Round 3 found the fast column update wrong (5.6e-3 rel-L2) once its
+    scheduling barrier was removed: the inline-asm pivot-row FMA read a v_dot2
+    result two instructions later, where gfx950 needs three wait states the
+    compiler inserts only for instructions it can see (tools/isa_hazards.py).
+    The FMA is compiler-visible now, so the barrier is a register knob only:
+    the build without it (libbmfr_fastnosb.so, -DBMFR_FAST_SCHED_BARRIER=0,
+    run in a child process) must give the default build's frames bit for bit
+    -- a schedule never changes an IEEE result -- and stay within north_star's
+    1e-4 of the exact path."""
+    import os
+    import subprocess
+    import sys
+
+    import numpy as np
+    W, H, n = 200, 136, 20
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "bmfr_amd", "libbmfr_fastnosb.so")):
+        pytest.fail("libbmfr_fastnosb.so missing (__graft_entry__.build())")
+    out = tmp_path / "nosb.npy"
+    env = dict(os.environ, BMFR_LIB="fastnosb")
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "variant_frames.py"), str(W), str(H), str(n), "1",
+                        str(out)], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "BMFR_FAST_SCHED_BARRIER=0" in r.stdout, r.stdout
+    nosb = torch.from_numpy(np.load(out))
+    cfg, frames = frames_of(W, H, n)
+    fast = run_frames(cfg, frames)
+    exact = run_frames(bmfr_amd.BmfrConfig(image_width=W, image_height=H), frames)
+    for f in range(n):
+        got = fast[f]["result"].cpu()
+        assert same_bits(nosb[f], got), f"frame {f}: barrier-free build differs from the default build"
+        assert rel_l2(nosb[f], exact[f]["result"].cpu()) < TOL

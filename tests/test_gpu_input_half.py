@@ -23,14 +23,19 @@ def _bits(t: torch.Tensor) -> np.ndarray:
     return t.cpu().numpy().view(np.uint32)
 
 
+@pytest.mark.parametrize("fast_fit", [0, 1])
 @pytest.mark.parametrize("W,H,scaled,half_tmp", [
     (160, 96, bmfr_amd.SCALED_DEFAULT, 1),       # column-split K1, B = 13
     (160, 96, bmfr_amd.SCALED_THIRD_ORDER, 1),   # column-split K1, B = 16 (config 5's feature set)
     (128, 80, bmfr_amd.SCALED_DEFAULT, 0),       # row-split K1 (f32 tmp_data)
     (100, 72, bmfr_amd.SCALED_THIRD_ORDER, 0),
 ])
-def test_half_inputs_match_widened_f32(W, H, scaled, half_tmp, gpu):
-    base = dict(image_width=W, image_height=H, scaled=scaled, use_half_precision_in_tmp_data=half_tmp)
+def test_half_inputs_match_widened_f32(W, H, scaled, half_tmp, fast_fit, gpu):
+    """(fast_fit too: the fused update changes the fit's arithmetic, not how
+    the inputs are read, so half planes == widened planes bit for bit there
+    as well -- config 5's timed configuration.)"""
+    base = dict(image_width=W, image_height=H, scaled=scaled, use_half_precision_in_tmp_data=half_tmp,
+                fast_fit=fast_fit)
     den_h = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(**base, input_half=1))
     den_f = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(**base))
     n = W * H * 3

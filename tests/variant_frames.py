@@ -1,0 +1,31 @@
+"""Child process of tests/test_gpu_fast_fit.py: run W x H synthetic frames
+through the library variant BMFR_LIB names and save the frame outputs
+(float32, frames x W*H*3) to the .npy path given."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bmfr_amd  # noqa: E402
+
+
+def main(W, H, n, fast_fit, out):
+    cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, fast_fit=fast_fit)
+    den = bmfr_amd.Denoiser(cfg)
+    res = np.empty((n, W * H * 3), np.float32)
+    for f in range(n):
+        fr = bmfr_amd.synth_frame_device(W, H, f)
+        vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+        _, jit = bmfr_amd.synth_camera(W, H, f)
+        den.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, f)
+        res[f] = den.copy_output(torch.empty(W * H * 3, device="cuda")).cpu().numpy()
+    np.save(out, res)
+    print("build", bmfr_amd.build_id())
+
+
+if __name__ == "__main__":
+    main(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])
