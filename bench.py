@@ -143,6 +143,10 @@ def parse(argv=None):
     ap.add_argument("--sequence", action="store_true",
                     help="single GPU: the timed frames as one bmfr_process_sequence call (TAA of frame f beside "
                          "K1 of frame f+1) instead of one bmfr_process_frame per frame")
+    ap.add_argument("--exchange", choices=("native", "torch"), default="native",
+                    help="multi-GPU over RCCL: native = libbmfr's bmfr_exchange_run (pack + grouped ncclSend / "
+                         "ncclRecv + unpack, one C call per frame); torch = torch.distributed isend / irecv between "
+                         "libbmfr's pack / unpack (gloo rehearsals always use torch)")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="multi-GPU: exchange the halo before the frame instead of under K1's interior blocks")
     a = ap.parse_args(argv)
@@ -198,6 +202,20 @@ def pmc_traffic(workload: str):
 PROF_STRIDE = 10  # timed frames between two recorded with per-kernel events
 
 
+class NativeTransport:
+    """DistTransport's interface over libbmfr's native exchange (bmfr_exchange_run)."""
+
+    def __init__(self, x, comm):
+        self.x, self.comm = x, comm  # the communicator outlives the exchange
+
+    @property
+    def last_bytes(self):
+        return self.x.last_bytes
+
+    def exchange_ctx(self, denoiser, frame):
+        self.x.run(frame)
+
+
 def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, per_frame=False):
     """Denoise frames 0..warmup+steps-1 of the synthetic W x H sequence (this
     rank's tile of it); time the last `steps` frames.  Returns the timings,
@@ -228,7 +246,15 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         _, jit = bmfr_amd.synth_camera(W, H, f)
         cams.append((vp, jit))
     scratch = spin_up(a, cfg, local, frames, cams)  # its last frames still run under the warm-up frames
-    transport = tiling.DistTransport(grid, rank, dev, host_staging=backend != "nccl") if grid else None
+    transport = None
+    if grid:
+        # RCCL: libbmfr's native exchange (one C call per frame enqueues pack, the grouped
+        # ncclSend / ncclRecv batch and unpack); gloo (the one-GPU rehearsal) or
+        # --exchange torch: torch.distributed point-to-point between libbmfr's pack / unpack
+        transport = tiling.DistTransport(grid, rank, dev, host_staging=backend != "nccl")
+        if backend == "nccl" and a.exchange == "native":
+            comm_handle = tiling.RcclComm(world, rank, local)
+            transport = NativeTransport(tiling.NativeExchange(den, grid, rank, comm_handle), comm_handle)
     # Tiled: the halo exchange runs on its own stream while K1's interior
     # blocks (which need no halo) run on the compute stream
     # (bmfr_process_frame_interior / _border, include/bmfr.h).
@@ -372,7 +398,11 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         "psnr_in": psnr(tile_of(noisy_tm).cpu().numpy(), tile_of(clean).cpu().numpy()),
         "split": split,
     }
-    del frames, den, out, clean, noisy_tm, last, scratch
+    if isinstance(transport, NativeTransport):
+        torch.cuda.synchronize()
+        transport.x.close()
+        transport.comm.close()
+    del frames, den, out, clean, noisy_tm, last, scratch, transport
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return res
@@ -603,6 +633,7 @@ def main():
                        "frames_pipelined": world == 1 and a.sequence,
                        "parallelism": (f"tiles {tx}x{ty}, halo {a.halo} px, "
                                        f"{'RCCL' if backend == 'nccl' else backend} halo exchange"
+                                       f"{' (libbmfr bmfr_exchange_run)' if backend == 'nccl' and a.exchange == 'native' else ' (torch.distributed)'}"
                                        f"{' overlapped with interior blocks' if a.overlap else ''}")
                        if world > 1 else "single GPU"},
             "device_ms_per_frame": round(r["dev_ms"], 4),

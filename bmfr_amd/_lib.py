@@ -117,6 +117,17 @@ SIGNATURES = {
     "bmfr_set_profiling": (_I, [_P, _I, _I]),
     "bmfr_set_profiling_stride": (_I, [_P, _I]),
     "bmfr_get_profile": (_I, [_P, C.POINTER(FrameProfile), _I, C.POINTER(_I)]),
+    "bmfr_halo_plan": (_I, [C.POINTER(Config), C.POINTER(_I), _I, _I, _I, C.POINTER(_I), C.POINTER(_I),
+                            C.POINTER(_I), C.POINTER(_I), _I, C.POINTER(_I)]),
+    "bmfr_comm_unique_id": (_I, [C.c_char_p]),
+    "bmfr_comm_create": (_I, [C.c_char_p, _I, _I, _I, C.POINTER(_P)]),
+    "bmfr_comm_create_all": (_I, [_I, C.POINTER(_I), C.POINTER(_P)]),
+    "bmfr_comm_destroy": (_I, [_P]),
+    "bmfr_exchange_create": (_I, [_P, C.POINTER(Config), C.POINTER(_I), _I, _I, _P, C.POINTER(_P)]),
+    "bmfr_exchange_run": (_I, [_P, _P, _I]),
+    "bmfr_exchange_run_all": (_I, [C.POINTER(_P), _I, C.POINTER(_P), _I]),
+    "bmfr_exchange_bytes": (_I, [_P, _I, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "bmfr_exchange_destroy": (_I, [_P]),
     "bmfr_synth_camera": (None, [_I, _I, _I, _F16, _F2]),
     "bmfr_debug_stamps": (_I, [_P, _P, C.c_size_t]),  # include/bmfr_debug.h
     "bmfr_debug_sync": (_I, [_P, _I, _I]),  # include/bmfr_debug.h

@@ -382,3 +382,115 @@ def state_planes(denoiser) -> list:
     v = denoiser.state(previous=False)
     reg = denoiser.region
     return [Plane(getattr(v, name), reg, bpp) for name, bpp in STATE_PLANES]
+
+
+# ------------------------------------------- libbmfr's native exchange ----
+def native_plan(cfg, grid: TileGrid, rank: int, frame: int):
+    """bmfr_halo_plan (the C plan) in frame_plan's format: [(peer, send, recv)]."""
+    from . import _lib
+    lib = _lib.load()
+    c = dataclasses.replace(cfg, tile=grid.tile(rank), tile_halo=grid.halo).to_c()
+    tiles = (C.c_int * (4 * grid.ranks))(*[v for r in range(grid.ranks) for v in grid.tile(r)])
+    n = C.c_int()
+    _lib.check(lib.bmfr_halo_plan(C.byref(c), tiles, grid.ranks, rank, frame, None, None, None, None, 0,
+                                  C.byref(n)), "bmfr_halo_plan")
+    cap = 8 * grid.ranks
+    peers, sc, rc = (C.c_int * max(n.value, 1))(), (C.c_int * max(n.value, 1))(), (C.c_int * max(n.value, 1))()
+    recs = (C.c_int * (5 * cap))()
+    _lib.check(lib.bmfr_halo_plan(C.byref(c), tiles, grid.ranks, rank, frame, peers, sc, rc, recs, cap,
+                                  C.byref(n)), "bmfr_halo_plan")
+    out, k = [], 0
+    for i in range(n.value):
+        send = [tuple(recs[5 * (k + j):5 * (k + j) + 5]) for j in range(sc[i])]
+        k += sc[i]
+        recv = [tuple(recs[5 * (k + j):5 * (k + j) + 5]) for j in range(rc[i])]
+        k += rc[i]
+        out.append((peers[i], send, recv))
+    return out
+
+
+def _tiles_array(grid: TileGrid):
+    return (C.c_int * (4 * grid.ranks))(*[v for r in range(grid.ranks) for v in grid.tile(r)])
+
+
+class RcclComm:
+    """libbmfr's RCCL communicator for one rank (bmfr_comm_create); the
+    unique id travels over the torch.distributed group (gloo or nccl)."""
+
+    def __init__(self, world: int, rank: int, device: int):
+        import torch
+        import torch.distributed as dist
+
+        from . import _lib
+        self.lib = _lib.load()
+        uid = (C.c_char * 128)()
+        if rank == 0:
+            _lib.check(self.lib.bmfr_comm_unique_id(uid), "bmfr_comm_unique_id")
+        t = torch.tensor(list(bytes(uid)), dtype=torch.uint8)
+        if dist.get_backend() == "nccl":
+            t = t.cuda(device)
+        dist.broadcast(t, 0)
+        uid = (C.c_char * 128)(*t.cpu().tolist())
+        h = C.c_void_p()
+        _lib.check(self.lib.bmfr_comm_create(uid, world, rank, device, C.byref(h)), "bmfr_comm_create")
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self.lib.bmfr_comm_destroy(self.handle)
+            self.handle = None
+
+
+class NativeExchange:
+    """One rank's halo exchange inside libbmfr (bmfr_exchange_*): pack, the
+    grouped ncclSend / ncclRecv batch and unpack enqueued by ONE C call per
+    frame -- the per-frame host work of DistTransport.exchange_ctx (plan
+    lookup, P2POp lists, two pack / unpack calls) gone.  comm=None: an
+    in-process grid, driven by run_all."""
+
+    def __init__(self, denoiser, grid: TileGrid, rank: int, comm: RcclComm | None):
+        from . import _lib
+        self.lib = _lib.load()
+        self.grid, self.rank, self.comm = grid, rank, comm
+        h = C.c_void_p()
+        self._tiles = _tiles_array(grid)
+        _lib.check(self.lib.bmfr_exchange_create(denoiser.handle, C.byref(denoiser.cfg.to_c()), self._tiles,
+                                                 grid.ranks, rank, comm.handle if comm else None, C.byref(h)),
+                   "bmfr_exchange_create")
+        self.handle = h
+        self.last_bytes = (0, 0)
+
+    def bytes(self, frame: int):
+        s, r = C.c_size_t(), C.c_size_t()
+        self.lib.bmfr_exchange_bytes(self.handle, frame, C.byref(s), C.byref(r))
+        return s.value, r.value
+
+    def run(self, frame: int, stream=None) -> None:
+        import torch
+
+        from . import _lib
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        _lib.check(self.lib.bmfr_exchange_run(self.handle, s, frame), "bmfr_exchange_run")
+        self.last_bytes = self.bytes(frame)
+
+    @staticmethod
+    def run_all(exchanges, frame: int, streams=None) -> None:
+        import torch
+
+        from . import _lib
+        n = len(exchanges)
+        xs = (C.c_void_p * n)(*[x.handle.value for x in exchanges])
+        ss = streams or [torch.cuda.current_stream()] * n
+        st = (C.c_void_p * n)(*[s.cuda_stream for s in ss])
+        _lib.check(exchanges[0].lib.bmfr_exchange_run_all(xs, n, st, frame), "bmfr_exchange_run_all")
+
+    def close(self):
+        if self.handle:
+            self.lib.bmfr_exchange_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -68,6 +68,11 @@ struct Options {
     int half_tmp = USE_HALF_PRECISION_IN_TMP_DATA;
     int device = 0;
     unsigned seed = 0x424D4652;
+    // --tile-grid TXxTY: the frame sharded into tiles, one libbmfr context per
+    // tile, the halo exchanged by bmfr_exchange_run_all (RCCL between devices
+    // with --gpus N = tiles, device copies when every tile is on one GPU)
+    int tiles_x = 0, tiles_y = 0, tile_halo = 64, gpus = 1;
+    int fast_fit = 0;
 };
 
 void usage() {
@@ -86,7 +91,13 @@ void usage() {
         "  --features-not-scaled S --features-scaled S   feature lists as in bmfr.cpp:65-77\n"
         "  --half-tmp 0|1         USE_HALF_PRECISION_IN_TMP_DATA\n"
         "  --no-pipeline          synchronous uploads (as bmfr.cpp)\n"
-        "  --device I\n");
+        "  --device I\n"
+        "  --tile-grid TXxTY      shard each frame into TX x TY tiles (one context per tile, halo exchange\n"
+        "                         between frames: bmfr_exchange_run_all)\n"
+        "  --tile-halo PX         tile halo in pixels (default 64; >= 34 + the scene's motion per frame)\n"
+        "  --gpus N               tiles on N GPUs from --device on (N = 1: all on one GPU, device copies;\n"
+        "                         N = tiles: one GPU per tile, RCCL)\n"
+        "  --fast-fit             bmfr_config.fast_fit = 1\n");
 }
 
 bool parse_args(int argc, char** argv, Options& o) {
@@ -116,6 +127,15 @@ bool parse_args(int argc, char** argv, Options& o) {
         else if (a == "--no-pipeline") o.pipelined = false;
         else if (a == "--device") o.device = std::atoi(next("an index"));
         else if (a == "--seed") o.seed = (unsigned)std::strtoul(next("a number"), nullptr, 0);
+        else if (a == "--tile-grid") {
+            const char* g = next("TXxTY");
+            if (std::sscanf(g, "%dx%d", &o.tiles_x, &o.tiles_y) != 2 || o.tiles_x < 1 || o.tiles_y < 1) {
+                std::fprintf(stderr, "--tile-grid wants TXxTY, got %s\n", g);
+                return false;
+            }
+        } else if (a == "--tile-halo") o.tile_halo = std::atoi(next("pixels"));
+        else if (a == "--gpus") o.gpus = std::atoi(next("a count"));
+        else if (a == "--fast-fit") o.fast_fit = 1;
         else if (a == "-h" || a == "--help") {
             usage();
             std::exit(0);
@@ -285,6 +305,169 @@ double tonemap(float albedo_times_color) {  // bmfr.cl:851-856 (for the PSNR ref
 
 }  // namespace
 
+// [start, end) of part i of n split into `parts` near-equal runs, multiples of
+// 32 where possible (bmfr_amd/tiling.py _split: the same tiles as bench.py).
+void split(int n, int parts, int i, int& a, int& b) {
+    // std::nearbyint: ties to even, as Python's round()
+    auto edge = [&](int k) { return k == parts ? n : (int)std::nearbyint((double)n * k / parts / 32.0) * 32; };
+    a = edge(i);
+    b = edge(i + 1);
+}
+
+// The frame loop over a tile grid: frame 0 per tile, then per frame the
+// interior blocks of every tile, the halo exchange, the border blocks and
+// TAA (bmfr_process_frame_interior / bmfr_exchange_run_all /
+// bmfr_process_frame_border); each tile's output pixels are copied into the
+// host frame.  Host frames are full-size; a tile uploads its region.
+int run_tiled(const Options& o, const bmfr_config& base, const Camera& cam, const std::vector<std::vector<float>>& noisy,
+              const std::vector<std::vector<float>>& normals, const std::vector<std::vector<float>>& positions,
+              const std::vector<std::vector<float>>& albedos, std::vector<std::vector<float>>& out) {
+    const int W = o.width, H = o.height, F = o.frames, T = o.tiles_x * o.tiles_y;
+    if (o.gpus != 1 && o.gpus != T) {
+        std::fprintf(stderr, "--gpus must be 1 or the number of tiles (%d)\n", T);
+        return 1;
+    }
+    std::vector<int> tiles(4 * T);
+    for (int r = 0; r < T; ++r) {
+        int x0, x1, y0, y1;
+        split(W, o.tiles_x, r % o.tiles_x, x0, x1);
+        split(H, o.tiles_y, r / o.tiles_x, y0, y1);
+        tiles[4 * r] = x0, tiles[4 * r + 1] = y0, tiles[4 * r + 2] = x1 - x0, tiles[4 * r + 3] = y1 - y0;
+    }
+    struct Tile {
+        bmfr_config cfg;
+        bmfr_ctx* ctx = nullptr;
+        bmfr_sizes sz;
+        int device = 0;
+        hipStream_t stream = nullptr;
+        float* in[2][4] = {};  // current / previous region planes: noisy, normal, position, albedo
+        bmfr_exchange* x = nullptr;
+    };
+    std::vector<Tile> t(T);
+    std::vector<bmfr_comm*> comms(T, nullptr);
+    if (o.gpus == T && T > 1) {
+        std::vector<int> devs(T);
+        for (int r = 0; r < T; ++r) devs[r] = o.device + r;
+        BMFR_CHECK(bmfr_comm_create_all(T, devs.data(), comms.data()));
+    }
+    for (int r = 0; r < T; ++r) {
+        Tile& q = t[r];
+        q.cfg = base;
+        q.cfg.tile_x = tiles[4 * r], q.cfg.tile_y = tiles[4 * r + 1];
+        q.cfg.tile_width = tiles[4 * r + 2], q.cfg.tile_height = tiles[4 * r + 3];
+        q.cfg.tile_halo = o.tile_halo;
+        q.device = o.gpus == T ? o.device + r : o.device;
+        BMFR_CHECK(bmfr_create(&q.cfg, q.device, &q.ctx));
+        BMFR_CHECK(bmfr_get_sizes(q.ctx, &q.sz));
+        HIP_CHECK(hipSetDevice(q.device));
+        HIP_CHECK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+        for (auto& s : q.in)
+            for (auto& p : s) HIP_CHECK(hipMalloc(&p, q.sz.region_bytes));
+        BMFR_CHECK(bmfr_exchange_create(q.ctx, &q.cfg, tiles.data(), T, r, comms[r], &q.x));
+    }
+    std::printf("Processing %d frames (%dx%d) as %dx%d tiles, halo %d px, on %d GPU(s).\n", F, W, H, o.tiles_x,
+                o.tiles_y, o.tile_halo, o.gpus);
+    std::vector<bmfr_exchange*> xs(T);
+    std::vector<void*> streams(T);
+    for (int r = 0; r < T; ++r) xs[r] = t[r].x, streams[r] = t[r].stream;
+    size_t sent = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int f = 0; f < F; ++f) {
+        const int matrix_index = f == 0 ? 0 : f - 1;  // bmfr.cpp:440
+        std::vector<bmfr_frame_inputs> in(T);
+        for (int r = 0; r < T; ++r) {
+            Tile& q = t[r];
+            HIP_CHECK(hipSetDevice(q.device));
+            const bmfr_sizes& z = q.sz;
+            float** d = q.in[f & 1];
+            const std::vector<float>* src[4] = {&noisy[f], &normals[f], &positions[f], &albedos[f]};
+            for (int k = 0; k < 4; ++k)
+                HIP_CHECK(hipMemcpy2DAsync(d[k], (size_t)z.region_width * 12,
+                                           src[k]->data() + ((size_t)z.region_y * W + z.region_x) * 3, (size_t)W * 12,
+                                           (size_t)z.region_width * 12, z.region_height, hipMemcpyHostToDevice,
+                                           q.stream));
+            float** pv = q.in[(f + 1) & 1];
+            in[r] = {d[0], d[1], d[2], d[3], f > 0 ? pv[1] : nullptr, f > 0 ? pv[2] : nullptr};
+        }
+        if (f == 0) {
+            for (int r = 0; r < T; ++r)
+                BMFR_CHECK(bmfr_process_frame(t[r].ctx, t[r].stream, &in[r], &cam.matrices[16 * matrix_index],
+                                              &cam.offsets[2 * f], f));
+        } else {
+            for (int r = 0; r < T; ++r)
+                BMFR_CHECK(bmfr_process_frame_interior(t[r].ctx, t[r].stream, &in[r],
+                                                       &cam.matrices[16 * matrix_index], &cam.offsets[2 * f], f));
+            if (o.gpus == 1) {  // one stream carries the device copies: join every tile's stream onto it
+                for (int r = 1; r < T; ++r) {
+                    hipEvent_t e;
+                    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                    HIP_CHECK(hipEventRecord(e, t[r].stream));
+                    HIP_CHECK(hipStreamWaitEvent(t[0].stream, e, 0));
+                    HIP_CHECK(hipEventDestroy(e));
+                }
+            }
+            BMFR_CHECK(bmfr_exchange_run_all(xs.data(), T, streams.data(), f));
+            if (o.gpus == 1) {
+                hipEvent_t e;
+                HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                HIP_CHECK(hipEventRecord(e, t[0].stream));
+                for (int r = 1; r < T; ++r) HIP_CHECK(hipStreamWaitEvent(t[r].stream, e, 0));
+                HIP_CHECK(hipEventDestroy(e));
+            }
+            for (int r = 0; r < T; ++r)
+                BMFR_CHECK(bmfr_process_frame_border(t[r].ctx, t[r].stream, &in[r],
+                                                     &cam.matrices[16 * matrix_index], &cam.offsets[2 * f], f));
+            size_t s = 0;
+            for (int r = 0; r < T; ++r) {
+                size_t a = 0;
+                (void)bmfr_exchange_bytes(t[r].x, f, &a, nullptr);
+                s += a;
+            }
+            sent += s;
+        }
+        for (int r = 0; r < T; ++r) {  // the tile's pixels of the output (region row stride)
+            Tile& q = t[r];
+            const bmfr_sizes& z = q.sz;
+            const float* res = bmfr_output(q.ctx);
+            const int tx = tiles[4 * r], ty = tiles[4 * r + 1], tw = tiles[4 * r + 2], th = tiles[4 * r + 3];
+            HIP_CHECK(hipSetDevice(q.device));
+            HIP_CHECK(hipMemcpy2DAsync(out[f].data() + ((size_t)ty * W + tx) * 3, (size_t)W * 12,
+                                       res + ((size_t)(ty - z.region_y) * z.region_width + (tx - z.region_x)) * 3,
+                                       (size_t)z.region_width * 12, (size_t)tw * 12, th, hipMemcpyDeviceToHost,
+                                       q.stream));
+            // the region buffers of frame f are read again as frame f+1's previous planes
+            // and rewritten by frame f+2: finish the frame before its slot is reused
+        }
+        for (int r = 0; r < T; ++r) {
+            HIP_CHECK(hipSetDevice(t[r].device));
+            HIP_CHECK(hipStreamSynchronize(t[r].stream));
+        }
+    }
+    const double wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    int rc = 0;
+    for (int r = 0; r < T; ++r) {
+        unsigned over = 0;
+        const bmfr_status st = bmfr_halo_status(t[r].ctx, &over);
+        if (st != BMFR_OK) {
+            std::printf("tile %d: %s (%u px)\n", r, bmfr_status_string(st), over);
+            rc = 1;
+        }
+    }
+    std::printf("Tiled: %.3f ms/frame wall (synchronous per frame), halo %.2f MB sent per frame\n", wall_ms / F,
+                F > 1 ? sent / 1e6 / (F - 1) : 0.0);
+    for (int r = 0; r < T; ++r) {
+        Tile& q = t[r];
+        HIP_CHECK(hipSetDevice(q.device));
+        bmfr_exchange_destroy(q.x);
+        for (auto& s : q.in)
+            for (auto& p : s) (void)hipFree(p);
+        (void)hipStreamDestroy(q.stream);
+        bmfr_destroy(q.ctx);
+        if (comms[r]) bmfr_comm_destroy(comms[r]);
+    }
+    return rc;
+}
+
 int run(const Options& o) {
     const int W = o.width, H = o.height, F = o.frames;
     const size_t plane = (size_t)W * H * 3;
@@ -352,11 +535,13 @@ int run(const Options& o) {
         cfg.normal_limit_squared = cam.normal_limit_squared;
     }
 
+    cfg.fast_fit = o.fast_fit;
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, o.device));
     std::printf("Using device named: %s\n", prop.name);
+    const bool tiled = o.tiles_x > 0;
     bmfr_ctx* ctx = nullptr;
-    BMFR_CHECK(bmfr_create(&cfg, o.device, &ctx));
+    if (!tiled) BMFR_CHECK(bmfr_create(&cfg, o.device, &ctx));
 
     // ---- Loading input data (bmfr.cpp:254-307) ----
     std::printf("Loading input data.\n");
@@ -392,8 +577,23 @@ int run(const Options& o) {
     }
     if (error) {
         std::printf("One or more errors occurred during buffer loading\n");
-        bmfr_destroy(ctx);
+        if (ctx) bmfr_destroy(ctx);
         return 1;
+    }
+    if (tiled) {
+        const int rc = run_tiled(o, cfg, cam, noisy, normals, positions, albedos, out);
+        if (rc != 0) return rc;
+        bool err = false;
+        if (o.save) {
+#pragma omp parallel for
+            for (int f = 0; f < F; ++f) {
+                const std::string name = frame_file(o.output, f, o.exr ? ".exr" : ".png");
+                const int r = o.exr ? bmfr_exr_write_rgb(name.c_str(), W, H, out[f].data(), (size_t)W * 3, BMFR_EXR_ZIP)
+                                    : bmfr_png_write_rgb(name.c_str(), W, H, out[f].data(), (size_t)W * 3);
+                if (r != 0) err = true;
+            }
+        }
+        return err ? 1 : 0;
     }
 
     // ---- Device buffers: a ring of 3 input sets (frame f, f-1 as the

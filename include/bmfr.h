@@ -295,6 +295,56 @@ bmfr_status bmfr_halo_copy(bmfr_ctx *ctx, void *stream, const int *rects, int n,
  * depend on frame_number % 16 only. */
 bmfr_status bmfr_halo_need(const bmfr_config *cfg, int frame_number, int state_rect[4], int result_rect[4]);
 
+/* ---- Multi-GPU halo exchange (SURVEY.md 5 "Distributed communication
+ * backend", 8e; no reference counterpart: the reference drives one GPU,
+ * bmfr.cpp:183-191) ----
+ * A tile grid is ntiles rectangles tiles[4 r .. 4 r + 3] = {x, y, width,
+ * height} partitioning the frame; rank r runs a tiled context whose
+ * bmfr_config has tile_* = tile r (same tile_halo for every rank).
+ *
+ * bmfr_halo_plan: what rank `rank` exchanges before frame_number (host only):
+ * for each of the *n_peers neighbours, peers[k], then send_counts[k]
+ * bmfr_halo_copy records of its own tile that the neighbour's frame reads,
+ * then recv_counts[k] records of the neighbour's tile its own frame reads,
+ * all in `records` (5 ints each, at most max_records).  peers = records =
+ * NULL only counts.  Depends on frame_number % 16.  (bmfr_amd/tiling.py
+ * TileGrid.frame_plan is the same plan.) */
+bmfr_status bmfr_halo_plan(const bmfr_config *cfg, const int *tiles, int ntiles, int rank, int frame_number,
+    int *peers, int *send_counts, int *recv_counts, int *records, int max_records, int *n_peers);
+
+/* RCCL communicator of one rank (RCCL is loaded at run time; without it the
+ * calls return BMFR_ERROR_UNSUPPORTED).  One process per GPU: rank 0 makes
+ * the id (bmfr_comm_unique_id), every rank receives it out of band (e.g.
+ * torch.distributed / MPI broadcast) and calls bmfr_comm_create.  One
+ * process driving several GPUs: bmfr_comm_create_all (out[i] = rank i, on
+ * devices[i]). */
+typedef struct bmfr_comm bmfr_comm;
+bmfr_status bmfr_comm_unique_id(unsigned char id[128]);
+bmfr_status bmfr_comm_create(const unsigned char id[128], int nranks, int rank, int hip_device, bmfr_comm **out);
+bmfr_status bmfr_comm_create_all(int ndev, const int *devices, bmfr_comm **out);
+bmfr_status bmfr_comm_destroy(bmfr_comm *comm);
+
+/* The per-frame exchange of one rank: the plans of all 16 block-grid shifts
+ * and device send / receive buffers are made once here (cfg = the rank's
+ * context configuration; comm = its communicator, or NULL for an in-process
+ * grid).  bmfr_exchange_run, before frame_number > 0 of the context (after the
+ * previous frame, before bmfr_process_frame_border -- or before
+ * bmfr_process_frame), enqueues on `stream`: one pack kernel
+ * (bmfr_halo_copy), one ncclGroupStart / ncclSend / ncclRecv / ncclGroupEnd
+ * batch to the neighbours, one unpack kernel.  bmfr_exchange_run_all: every
+ * rank of a grid held by this process -- with communicators
+ * (bmfr_comm_create_all) all messages in one group, streams[i] rank i's
+ * stream; without, every context on one device and everything on
+ * streams[0] as device copies (single-GPU runs of a tiled grid). */
+typedef struct bmfr_exchange bmfr_exchange;
+bmfr_status bmfr_exchange_create(bmfr_ctx *ctx, const bmfr_config *cfg, const int *tiles, int ntiles, int rank,
+    bmfr_comm *comm, bmfr_exchange **out);
+bmfr_status bmfr_exchange_run(bmfr_exchange *x, void *stream, int frame_number);
+bmfr_status bmfr_exchange_run_all(bmfr_exchange *const *xs, int n, void *const *streams, int frame_number);
+/* Bytes rank x sends / receives before frame_number. */
+bmfr_status bmfr_exchange_bytes(const bmfr_exchange *x, int frame_number, size_t *sent, size_t *received);
+bmfr_status bmfr_exchange_destroy(bmfr_exchange *x);
+
 /* Tiled contexts: waits for the last enqueued frame and returns
  * BMFR_ERROR_HALO_EXCEEDED if any frame since frame 0 read reprojection taps
  * past its valid state (see tile_halo), BMFR_OK otherwise; *overshoot

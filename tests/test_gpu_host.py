@@ -71,3 +71,18 @@ def test_device_renderer_matches_host_renderer(gpu):
         for k in ("normals", "positions", "albedo"):
             assert d[k].cpu().numpy().tobytes() == h[k].reshape(-1).tobytes(), (f, k)
         np.testing.assert_allclose(d["noisy"].cpu().numpy(), h["noisy"].reshape(-1), rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("grid,halo", [("2x2", 40), ("4x1", 38)])
+def test_host_tile_grid_matches_untiled(tmp_path, grid, halo, gpu):
+    """bmfr_host --tile-grid: the frame sharded into tiles, one context per
+    tile, the halo exchanged by bmfr_exchange_run_all (all tiles on one GPU:
+    device copies), == the untiled host run bit for bit, every frame."""
+    size = ["--width", str(W), "--height", str(H), "--frames", str(F), "--synthetic", "--exr"]
+    _run([*size, "--output", str(tmp_path / "full_")], tmp_path)
+    log = _run([*size, "--output", str(tmp_path / "tile_"), "--tile-grid", grid, "--tile-halo", str(halo)], tmp_path)
+    assert "Tiled:" in log, log
+    for f in range(F):
+        a, b = _read(tmp_path / f"tile_{f}.exr"), _read(tmp_path / f"full_{f}.exr")
+        bad = a.view(np.uint32) != b.view(np.uint32)
+        assert not bad.any(), (grid, f, int(bad.sum()), np.argwhere(bad)[:3].tolist())

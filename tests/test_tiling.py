@@ -187,3 +187,35 @@ def test_halo_rects_partition_region_minus_tile(region, tile):
     m[y:y + h, x:x + w] += 1
     rx, ry, rw, rh = region
     assert (m[ry:ry + rh, rx:rx + rw] == 1).all() and m.sum() == rw * rh
+
+
+@pytest.mark.parametrize("W,H,tx,ty,halo", [(7680, 4320, 4, 2, 64), (7680, 4320, 2, 4, 64), (7680, 4320, 2, 2, 64),
+                                            (7680, 4320, 2, 1, 64), (480, 288, 4, 2, 38), (352, 224, 2, 1, 48)])
+def test_native_plan_equals_frame_plan(W, H, tx, ty, halo):
+    """libbmfr's bmfr_halo_plan (the plan bmfr_exchange_* sends on) is
+    TileGrid.frame_plan record for record, for every rank and all 16
+    block-grid shifts."""
+    import bmfr_amd
+    from bmfr_amd import tiling
+    cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H)
+    g = tiling.TileGrid(W, H, tx, ty, halo=halo)
+    for r in range(g.ranks):
+        for f in range(16):
+            want = [(p, [tuple(x) for x in s], [tuple(x) for x in q]) for p, s, q in g.frame_plan(r, f)]
+            assert tiling.native_plan(cfg, g, r, f) == want, (r, f)
+
+
+def test_native_plan_rejects_bad_grids():
+    import ctypes as C
+
+    import bmfr_amd
+    from bmfr_amd import _lib
+    lib = _lib.load()
+    c = bmfr_amd.BmfrConfig(image_width=256, image_height=128, tile=(0, 0, 128, 128), tile_halo=40).to_c()
+    n = C.c_int()
+    for tiles, rank in [([0, 0, 128, 128, 100, 0, 156, 128], 0),   # overlapping tiles
+                        ([0, 0, 128, 128], 0),                     # do not cover the frame
+                        ([0, 0, 128, 128, 128, 0, 128, 128], 2)]:  # rank out of range
+        arr = (C.c_int * len(tiles))(*tiles)
+        assert lib.bmfr_halo_plan(C.byref(c), arr, len(tiles) // 4, rank, 0, None, None, None, None, 0,
+                                  C.byref(n)) == 1
