@@ -155,7 +155,9 @@ def check_build_id(lib: C.CDLL, path: str) -> str:
     lib.bmfr_build_id.restype = C.c_char_p
     got = lib.bmfr_build_id().decode()
     want = _build.source_hash()
-    if got.split("+")[0] != want:
+    # BMFR_ALLOW_FOREIGN_BUILD=1: A/B timing of a library built from another
+    # revision's sources (tools/ab.py build-rev); never set by tests or bench.py
+    if got.split("+")[0] != want and os.environ.get("BMFR_ALLOW_FOREIGN_BUILD") != "1":
         raise StaleLibraryError(f"{path} was built from other sources (build id {got[:16]}..., tree "
                                 f"{want[:16]}...): rebuild it (__graft_entry__.build())")
     if "BMFR_PROBE" in got and os.environ.get("BMFR_ALLOW_PROBE") != "1":

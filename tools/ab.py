@@ -2,6 +2,7 @@
 """A/B timing of libbmfr builds on the GPU.
 
   build (here):   python tools/ab.py build NAME="-DFLAG=1 ..." ...   -> bmfr_amd/libbmfr_NAME.so
+                  python tools/ab.py build-rev NAME=GITREV ...         (the library of another revision)
   time (GPU box): python tools/ab.py time [W H] NAME ...             ("base" = libbmfr.so)
 
 Each timing runs in its own process (BMFR_LIB selects the library): frames
@@ -29,6 +30,39 @@ def build(specs):
             print(lib)
 
 
+def build_rev(specs):
+    """NAME=REV: libbmfr_NAME.so from the library sources of git revision REV
+    (csrc/ + include/, the build id of that tree), for A/B timing against
+    the working tree (timed with BMFR_ALLOW_FOREIGN_BUILD=1)."""
+    import shutil
+    import tempfile
+    from bmfr_amd import _build as b
+    for spec in specs:
+        name, rev = spec.split("=", 1)
+        with tempfile.TemporaryDirectory() as d:
+            subprocess.run(f"git -C {ROOT} archive {rev} bmfr_amd/csrc include | tar -x -C {d}", shell=True,
+                           check=True)
+            objdir = os.path.join(d, "obj")
+            os.makedirs(objdir)
+            csrc = os.path.join(d, "bmfr_amd", "csrc")
+            srcs = sorted(f for f in os.listdir(csrc) if f.endswith(".hip"))
+            with open(os.path.join(objdir, "bmfr_build_id.h"), "w") as f:
+                f.write(f'#define BMFR_BUILD_ID "rev-{rev}"\n')
+
+            def one(src):
+                obj = os.path.join(objdir, src.replace(".hip", ".o"))
+                subprocess.run([b.HIPCC, *b.FLAGS, "-I", objdir, "-c", os.path.join(csrc, src), "-o", obj],
+                               check=True)
+                return obj
+            with cf.ThreadPoolExecutor(max_workers=len(srcs)) as ex:
+                objs = list(ex.map(one, srcs))
+            out = os.path.join(ROOT, "bmfr_amd", f"libbmfr_{name}.so")
+            subprocess.run([b.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs, "-ldl"],
+                           check=True)
+            shutil.move(out + ".tmp", out)
+            print(out)
+
+
 def time_one(W, H, frames=45, first=5):
     import numpy as np
     import torch
@@ -52,7 +86,7 @@ def time_all(W, H, names, rounds=2):
     res = {n: [] for n in names}
     for _ in range(rounds):
         for n in names:
-            env = dict(os.environ, BMFR_LIB="" if n == "base" else n)
+            env = dict(os.environ, BMFR_LIB="" if n == "base" else n, BMFR_ALLOW_FOREIGN_BUILD="1")
             out = subprocess.run([sys.executable, __file__, "one", str(W), str(H)], env=env, capture_output=True,
                                  text=True, timeout=300)
             line = [x for x in out.stdout.splitlines() if x.startswith("RESULT")]
@@ -72,6 +106,8 @@ if __name__ == "__main__":
     cmd = sys.argv[1]
     if cmd == "build":
         build(sys.argv[2:])
+    elif cmd == "build-rev":
+        build_rev(sys.argv[2:])
     elif cmd == "one":
         time_one(int(sys.argv[2]), int(sys.argv[3]))
     else:
