@@ -577,7 +577,9 @@ struct WaveFit {
         });
         if (W == 0 && l < 3) L.R[l] = 32.f;  // R(0,0) = |column 0|
 
+#ifndef BMFR_PROBE_K1_NOQR  // timing probe (wrong results): no Householder steps
         steps(a, L, W, l, noise, pre, noise2, std::make_integer_sequence<int, NF>{});
+#endif
 
         // Right-hand side: rows 0..B-4 of the colour columns (bmfr.cl:596-600).
         sfor<NSL>([&](auto K) {

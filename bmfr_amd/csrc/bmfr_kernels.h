@@ -341,11 +341,20 @@ __device__ __forceinline__ NoisyTaps<IN> noisy_taps_issue(const Params& P, const
             const int sx = ix + (i & 1), sy = iy + (i >> 1);
             tp.inb |= (uint32_t)(sx >= 0 && sy >= 0 && sx < P.width && sy < P.height) << i;
             const uint32_t s = pix(P, clamp_rx(P, sx), clamp_ry(P, sy));
+#ifdef BMFR_PROBE_K1_NOTAPS  // timing probe (wrong results): no previous-frame tap loads
+            (void)s;
+            tp.pp[i] = c.wp;
+            tp.pn[i] = c.nrm;
+            tp.pc[i] = f3{pfx, pfy, 0.f};
+            tp.spu[i] = i;
+            if (FILT) tp.pa[i] = f3{pfy, pfx, 0.f};
+#else
             tp.pp[i] = ld3raw<IN>(in.p_prev, s);
             tp.pn[i] = ld3raw<IN>(in.n_prev, s);
             tp.pc[i] = ld3(in.noisy_prev, s);
             tp.spu[i] = ld_px(in.spp_prev, s);
             if (FILT) tp.pa[i] = ld3(acc_prev, s);  // same taps (bmfr.cl:801-832)
+#endif
         }
     }
     return tp;

@@ -184,13 +184,23 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
     // Previous-frame taps before the tone map: their latency hides under it.
     f3 taps[KN][4];
 #pragma unroll
-    for (int k = 0; k < KN; ++k) taa_load_taps(P, pf[k], T.prev_frame, taps[k]);
+    for (int k = 0; k < KN; ++k) {
+#ifdef BMFR_PROBE_K2_NOTAPS  // timing probe (wrong results): no previous-frame taps
+        taps[k][0] = taps[k][1] = taps[k][2] = taps[k][3] = f3{pf[k].x, pf[k].y, 0.f};
+#else
+        taa_load_taps(P, pf[k], T.prev_frame, taps[k]);
+#endif
+    }
     __syncthreads();  // the powr tables are in LDS
 #pragma unroll
     for (int k = 0; k <= KN; ++k) {
         if (k == KN && t >= RING) break;
         const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + RP * k + 1 : hy;
+#ifdef BMFR_PROBE_K2_NOTONE  // timing probe (wrong results): no tone map
+        { const f3 a = widen(al[k]); v[k] = f3{v[k].x * a.x, v[k].y * a.y, v[k].z * a.z}; }
+#else
         v[k] = tone_map(P, widen(al[k]), v[k], sE, sRP);
+#endif
         const f3 yc = rgb_to_ycocg(v[k]);
         Y[ly * HW + lx] = make_float4(yc.x, yc.y, yc.z, 0.f);
     }
@@ -209,8 +219,15 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
                 const float4 q = Y[c + (j / 3 - 1) * HW + (j % 3 - 1)];
                 nb[j] = f3{q.x, q.y, q.z};
             }
+#ifdef BMFR_PROBE_K2_NORESOLVE  // timing probe (wrong results): no TAA resolve
+            f3 r = v[k];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) r = f3{r.x + nb[j].x, r.y + nb[j].y, r.z + nb[j].z};
+            r = f3{r.x + taps[k][0].x + taps[k][3].y, r.y, r.z};
+#else
             const f3 r = edge ? taa_resolve<true>(P, x, y, v[k], pf[k], nb, taps[k], T.frame)
                               : taa_resolve<false>(P, x, y, v[k], pf[k], nb, taps[k], T.frame);
+#endif
             st3(T.result, pix(P, x, y), r);
         }
     }

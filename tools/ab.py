@@ -86,7 +86,8 @@ def time_all(W, H, names, rounds=2):
     res = {n: [] for n in names}
     for _ in range(rounds):
         for n in names:
-            env = dict(os.environ, BMFR_LIB="" if n == "base" else n, BMFR_ALLOW_FOREIGN_BUILD="1")
+            env = dict(os.environ, BMFR_LIB="" if n == "base" else n, BMFR_ALLOW_FOREIGN_BUILD="1",
+                       BMFR_ALLOW_PROBE="1")
             out = subprocess.run([sys.executable, __file__, "one", str(W), str(H)], env=env, capture_output=True,
                                  text=True, timeout=300)
             line = [x for x in out.stdout.splitlines() if x.startswith("RESULT")]
