@@ -256,19 +256,26 @@ struct NoisyCur {
     int px, py;
     bool owner;
 };
-template <class IN = float>
+// COLOUR = false: position and normal only (c.cur left for the caller).
+// Margin-grid item (gx, gy): its (mirrored) image pixel and whether it owns
+// it (bmfr.cl:310-317).
+__device__ __forceinline__ void item_pixel(const Params& P, int gx, int gy, int frame, int& px, int& py, bool& owner) {
+    const int2 off = kBlockOffsets[frame & 15];
+    const int ux = gx - kEdge / 2 + off.x, uy = gy - kEdge / 2 + off.y;
+    px = mirror(ux, P.width);
+    py = mirror(uy, P.height);
+    owner = ux >= 0 && ux < P.width && uy >= 0 && uy < P.height;
+}
+
+template <class IN = float, bool COLOUR = true>
 __device__ __forceinline__ NoisyCur<IN> noisy_load_current(const Params& P, const NoisyInputs& in, int gx, int gy,
                                                            int frame) {
     NoisyCur<IN> c;
-    const int2 off = kBlockOffsets[frame & 15];
-    const int ux = gx - kEdge / 2 + off.x, uy = gy - kEdge / 2 + off.y;
-    c.px = mirror(ux, P.width);
-    c.py = mirror(uy, P.height);
-    c.owner = ux >= 0 && ux < P.width && uy >= 0 && uy < P.height;
+    item_pixel(P, gx, gy, frame, c.px, c.py, c.owner);
     const uint32_t lin = pix(P, c.px, c.py);
     c.wp = ld3raw<IN>(in.p_cur, lin);
     c.nrm = ld3raw<IN>(in.n_cur, lin);
-    c.cur = ld3raw<IN>(in.noisy_cur, lin);
+    if constexpr (COLOUR) c.cur = ld3raw<IN>(in.noisy_cur, lin);
     return c;
 }
 
@@ -290,6 +297,71 @@ struct NoisyTaps {
 };
 
 
+// The reprojection of one item (bmfr.cl:343-372): the previous-frame pixel
+// position pf, the top-left bilinear tap (ix, iy) -- clamped in float first,
+// so a far-off reprojection cannot overflow int --, the four tap weights,
+// which taps lie inside the image (bit i: tap (ix + (i & 1), iy + (i >> 1)))
+// and, tiled contexts, how far the in-image taps reach past the valid state.
+// The bilinear tap weights at pf (bmfr.cl:359-372).
+__device__ __forceinline__ void bilinear_weights(float pfx, float pfy, float (&wts)[4]) {
+    const float fx = pfx - floorf(pfx), fy = pfy - floorf(pfy);
+    const float omx = 1.f - fx, omy = 1.f - fy;
+    wts[0] = omx * omy;
+    wts[1] = fx * omy;
+    wts[2] = omx * fy;
+    wts[3] = fx * fy;
+}
+
+struct Reproj {
+    float pfx, pfy;
+    int ix, iy;
+    float wts[4];
+    uint32_t inb;
+    int over;
+};
+__device__ __forceinline__ Reproj reproject(const Params& P, const Camera& cam, const f3& wp, int px, int py) {
+    Reproj r;
+    const float* M = cam.m;
+    float u = dot4(M[0], M[4], M[8], M[12], wp.x, wp.y, wp.z, 1.f);
+    float v = dot4(M[1], M[5], M[9], M[13], wp.x, wp.y, wp.z, 1.f);
+    const float w = dot4(M[3], M[7], M[11], M[15], wp.x, wp.y, wp.z, 1.f);
+    const float rw = 1.f / w;
+    u = div_shared(u, w, rw);
+    v = div_shared(v, w, rw);
+    u = u + 1.f;
+    v = v + 1.f;
+    u = u / 2.f;
+    v = v / 2.f;
+    const float pfx = u * (float)P.width - cam.jx;
+    const float pfy = v * (float)P.height - (1 - cam.jy);
+    r.pfx = pfx;
+    r.pfy = pfy;
+    const float flx = floorf(pfx), fly = floorf(pfy);
+    const int ix = (int)fminf(fmaxf(flx, -2.f), (float)P.width + 1.f);
+    const int iy = (int)fminf(fmaxf(fly, -2.f), (float)P.height + 1.f);
+    r.ix = ix;
+    r.iy = iy;
+    bilinear_weights(pfx, pfy, r.wts);
+    r.over = 0;
+    if (P.check_reach) {  // the in-image taps span [x0, x1] x [y0, y1]
+        const int x0 = max(ix, 0), x1 = min(ix + 1, P.width - 1);
+        const int y0 = max(iy, 0), y1 = min(iy + 1, P.height - 1);
+        // a tile pixel's taps also read the previous TAA output (in K2)
+        const bool tpx = px >= P.tx0 && px < P.tx1 && py >= P.ty0 && py < P.ty1;
+        const int vx0 = tpx ? P.wx0 : P.vx0, vx1 = tpx ? P.wx1 : P.vx1;
+        const int vy0 = tpx ? P.wy0 : P.vy0, vy1 = tpx ? P.wy1 : P.vy1;
+        if (x0 <= x1 && y0 <= y1)
+            r.over = max(max(max(vx0 - x0, x1 - (vx1 - 1)), max(vy0 - y0, y1 - (vy1 - 1))), 0);
+    }
+    r.inb = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int sx = ix + (i & 1), sy = iy + (i >> 1);
+        r.inb |= (uint32_t)(sx >= 0 && sy >= 0 && sx < P.width && sy < P.height) << i;
+    }
+    return r;
+}
+
 template <bool FILT = false, class IN = float>
 __device__ __forceinline__ NoisyTaps<IN> noisy_taps_issue(const Params& P, const NoisyInputs& in, const Camera& cam,
                                                          const NoisyCur<IN>& c, int frame,
@@ -300,54 +372,22 @@ __device__ __forceinline__ NoisyTaps<IN> noisy_taps_issue(const Params& P, const
     tp.over = 0;
     tp.inb = 0;
     if (frame > 0) {
-        const f3 wp = widen(c.wp);
-        const float* M = cam.m;
-        float u = dot4(M[0], M[4], M[8], M[12], wp.x, wp.y, wp.z, 1.f);
-        float v = dot4(M[1], M[5], M[9], M[13], wp.x, wp.y, wp.z, 1.f);
-        const float w = dot4(M[3], M[7], M[11], M[15], wp.x, wp.y, wp.z, 1.f);
-        const float rw = 1.f / w;
-        u = div_shared(u, w, rw);
-        v = div_shared(v, w, rw);
-        u = u + 1.f;
-        v = v + 1.f;
-        u = u / 2.f;
-        v = v / 2.f;
-        const float pfx = u * (float)P.width - cam.jx;
-        const float pfy = v * (float)P.height - (1 - cam.jy);
-        tp.pfx = pfx;
-        tp.pfy = pfy;
-        const float flx = floorf(pfx), fly = floorf(pfy);
-        // Clamp before converting: a far-off reprojection must not overflow int.
-        const int ix = (int)fminf(fmaxf(flx, -2.f), (float)P.width + 1.f);
-        const int iy = (int)fminf(fmaxf(fly, -2.f), (float)P.height + 1.f);
-        const float fx = pfx - flx, fy = pfy - fly;
-        const float omx = 1.f - fx, omy = 1.f - fy;
-        tp.wts[0] = omx * omy;
-        tp.wts[1] = fx * omy;
-        tp.wts[2] = omx * fy;
-        tp.wts[3] = fx * fy;
-        if (P.check_reach) {  // the in-image taps span [x0, x1] x [y0, y1]
-            const int x0 = max(ix, 0), x1 = min(ix + 1, P.width - 1);
-            const int y0 = max(iy, 0), y1 = min(iy + 1, P.height - 1);
-            // a tile pixel's taps also read the previous TAA output (in K2)
-            const bool tpx = c.px >= P.tx0 && c.px < P.tx1 && c.py >= P.ty0 && c.py < P.ty1;
-            const int vx0 = tpx ? P.wx0 : P.vx0, vx1 = tpx ? P.wx1 : P.vx1;
-            const int vy0 = tpx ? P.wy0 : P.vy0, vy1 = tpx ? P.wy1 : P.vy1;
-            if (x0 <= x1 && y0 <= y1)
-                tp.over = max(max(max(vx0 - x0, x1 - (vx1 - 1)), max(vy0 - y0, y1 - (vy1 - 1))), 0);
-        }
+        const Reproj r = reproject(P, cam, widen(c.wp), c.px, c.py);
+        tp.pfx = r.pfx;
+        tp.pfy = r.pfy;
+        tp.over = r.over;
+        tp.inb = r.inb;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int sx = ix + (i & 1), sy = iy + (i >> 1);
-            tp.inb |= (uint32_t)(sx >= 0 && sy >= 0 && sx < P.width && sy < P.height) << i;
-            const uint32_t s = pix(P, clamp_rx(P, sx), clamp_ry(P, sy));
+            tp.wts[i] = r.wts[i];
+            const uint32_t s = pix(P, clamp_rx(P, r.ix + (i & 1)), clamp_ry(P, r.iy + (i >> 1)));
 #ifdef BMFR_PROBE_K1_NOTAPS  // timing probe (wrong results): no previous-frame tap loads
             (void)s;
             tp.pp[i] = c.wp;
             tp.pn[i] = c.nrm;
-            tp.pc[i] = f3{pfx, pfy, 0.f};
+            tp.pc[i] = f3{r.pfx, r.pfy, 0.f};
             tp.spu[i] = i;
-            if (FILT) tp.pa[i] = f3{pfy, pfx, 0.f};
+            if (FILT) tp.pa[i] = f3{r.pfy, r.pfx, 0.f};
 #else
             tp.pp[i] = ld3raw<IN>(in.p_prev, s);
             tp.pn[i] = ld3raw<IN>(in.n_prev, s);
@@ -360,45 +400,57 @@ __device__ __forceinline__ NoisyTaps<IN> noisy_taps_issue(const Params& P, const
     return tp;
 }
 
-template <bool FILT = false, class IN = float>
-__device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const NoisyCur<IN>& c,
-                                                      const NoisyTaps<IN>& tp, int frame) {
+// The acceptance half of noisy_taps_finish (bmfr.cl:380-404): bit i set when
+// tap i is inside the image and its previous position and normal are close
+// enough to the pixel's current ones.
+template <class IN = float>
+__device__ __forceinline__ uint32_t taps_accept(const Params& P, const f3& wp, const f3& nrm, const In3<IN> (&pp)[4],
+                                                const In3<IN> (&pn)[4], uint32_t inb) {
+    uint32_t accept = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f3 q = widen(pp[i]), m = widen(pn[i]);
+        const f3 d{q.x - wp.x, q.y - wp.y, q.z - wp.z};
+        const f3 dn{m.x - nrm.x, m.y - nrm.y, m.z - nrm.z};
+        if ((inb & (1u << i)) && dot3(d, d) < P.position_limit_sq && dot3(dn, dn) < P.normal_limit_sq)
+            accept |= 1u << i;
+    }
+    return accept;
+}
+
+// The accumulation half (bmfr.cl:405-445, and with FILT accumulate_filtered_
+// data's sums at the same taps, bmfr.cl:786-842): the accepted taps' colours,
+// spp and filtered colours weighed and blended.  o.n / o.p are left to the
+// caller.
+template <bool FILT = false>
+__device__ __forceinline__ NoisyItem taps_blend(const Params& P, const f3& cur, uint32_t accept, const float (&wts)[4],
+                                                const f3 (&pc)[4], const uint32_t (&spu)[4], const f3 (&pa)[4],
+                                                float pfx, float pfy, int over, uint32_t lin, bool owner, int frame) {
     NoisyItem o;
-    o.owner = c.owner;
-    o.lin = pix(P, c.px, c.py);
-    const f3 wp = widen(c.wp), nrm = widen(c.nrm), cur = widen(c.cur);
-    o.n = nrm;
-    o.p = wp;
-    uint8_t accept = 0;
+    o.owner = owner;
+    o.lin = lin;
     float alpha = 1.f;
     f3 prev{0.f, 0.f, 0.f};
     float sample_spp = 0.f;
     o.prev_f = f3{0.f, 0.f, 0.f};
     o.alpha_f = 1.f;
     o.prev_f_divided = false;
-    o.over = tp.over;
+    o.over = over;
     float tap_total = 0.f;
     if (frame > 0) {
         float total = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {  // bmfr.cl:374-419
-            const f3 pp = widen(tp.pp[i]), pn = widen(tp.pn[i]);
-            const f3& pci = tp.pc[i];
-            const uint32_t spi = tp.spu[i];
-            const f3& pai = tp.pa[i];
-            const f3 d{pp.x - wp.x, pp.y - wp.y, pp.z - wp.z};
-            const f3 dn{pn.x - nrm.x, pn.y - nrm.y, pn.z - nrm.z};
-            if ((tp.inb & (1u << i)) && dot3(d, d) < P.position_limit_sq && dot3(dn, dn) < P.normal_limit_sq) {
-                accept |= (uint8_t)(1 << i);
-                sample_spp = sample_spp + tp.wts[i] * (float)spi;
-                prev.x = prev.x + tp.wts[i] * pci.x;
-                prev.y = prev.y + tp.wts[i] * pci.y;
-                prev.z = prev.z + tp.wts[i] * pci.z;
-                total = total + tp.wts[i];
+            if (accept & (1u << i)) {
+                sample_spp = sample_spp + wts[i] * (float)spu[i];
+                prev.x = prev.x + wts[i] * pc[i].x;
+                prev.y = prev.y + wts[i] * pc[i].y;
+                prev.z = prev.z + wts[i] * pc[i].z;
+                total = total + wts[i];
                 if (FILT) {  // accumulate_filtered_data's sums: same weights, same order
-                    o.prev_f.x = o.prev_f.x + tp.wts[i] * pai.x;
-                    o.prev_f.y = o.prev_f.y + tp.wts[i] * pai.y;
-                    o.prev_f.z = o.prev_f.z + tp.wts[i] * pai.z;
+                    o.prev_f.x = o.prev_f.x + wts[i] * pa[i].x;
+                    o.prev_f.y = o.prev_f.y + wts[i] * pa[i].y;
+                    o.prev_f.z = o.prev_f.z + wts[i] * pa[i].z;
                 }
             }
         }
@@ -425,10 +477,22 @@ __device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const No
     }
     const float beta = 1.f - alpha;
     o.color = f3{alpha * cur.x + beta * prev.x, alpha * cur.y + beta * prev.y, alpha * cur.z + beta * prev.z};
-    o.pfx = tp.pfx;
-    o.pfy = tp.pfy;
-    o.accept = accept;
+    o.pfx = pfx;
+    o.pfy = pfy;
+    o.accept = (uint8_t)accept;
     o.spp = new_spp;
+    return o;
+}
+
+template <bool FILT = false, class IN = float>
+__device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const NoisyCur<IN>& c,
+                                                      const NoisyTaps<IN>& tp, int frame) {
+    const f3 wp = widen(c.wp), nrm = widen(c.nrm), cur = widen(c.cur);
+    const uint32_t accept = frame > 0 ? taps_accept<IN>(P, wp, nrm, tp.pp, tp.pn, tp.inb) : 0u;
+    NoisyItem o = taps_blend<FILT>(P, cur, accept, tp.wts, tp.pc, tp.spu, tp.pa, tp.pfx, tp.pfy, tp.over,
+                                   pix(P, c.px, c.py), c.owner, frame);
+    o.n = nrm;
+    o.p = wp;
     return o;
 }
 
