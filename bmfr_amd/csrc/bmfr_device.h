@@ -62,6 +62,37 @@ __device__ __forceinline__ void st2_coh(CohPlane r, uint32_t i, float2 v) {
     __builtin_amdgcn_raw_buffer_store_b64(u2{__float_as_uint(v.x), __float_as_uint(v.y)}, r, i * 8u, 0, kSc1);
 }
 
+// Stores only some lanes perform, without a branch: raw buffer stores whose
+// discarded lanes get an out-of-range offset (the buffer range check drops
+// the write; a plane is far below 4 GiB, validate() in bmfr_capi.hip).  A
+// store inside a divergent branch makes the compiler's s_waitcnt for an OLDER
+// load after the branch conservative -- the count must hold on the path that
+// skipped the stores, so it waits for the stores' acknowledgement too (K1's
+// phase 1: each item's owner stores held up the next item's reprojection
+// until they were written back).  Issued on every path, they are counted
+// exactly.  `sc1`: the cache policy of the device-coherent hand-off (COH).
+typedef __amdgpu_buffer_rsrc_t DropPlane;
+__device__ __forceinline__ DropPlane drop_plane(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+constexpr uint32_t kDropOff = 0x80000000u;  // any offset past the range
+template <int AUX = 0>
+__device__ __forceinline__ void st3_drop(DropPlane r, uint32_t i, bool keep, f3 v) {
+    typedef unsigned u3 __attribute__((ext_vector_type(3)));
+    __builtin_amdgcn_raw_buffer_store_b96(u3{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z)}, r,
+                                          keep ? i * 12u : kDropOff, 0, AUX);
+}
+template <int AUX = 0>
+__device__ __forceinline__ void st2_drop(DropPlane r, uint32_t i, bool keep, float2 v) {
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(u2{__float_as_uint(v.x), __float_as_uint(v.y)}, r,
+                                          keep ? i * 8u : kDropOff, 0, AUX);
+}
+template <int AUX = 0>
+__device__ __forceinline__ void st1_drop(DropPlane r, uint32_t i, bool keep, uint8_t v) {
+    __builtin_amdgcn_raw_buffer_store_b8(v, r, keep ? i : kDropOff, 0, AUX);
+}
+
 // Plane elements by pixel index i.  The address is the plane's base (a kernel
 // argument: uniform, in SGPRs) plus a 32-bit byte offset (one VGPR) -- the
 // SGPR-base form of the global memory instructions -- so the planes read at

@@ -349,12 +349,10 @@ __device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K
         const uint32_t bits = (uint32_t)it.owner | ((uint32_t)it.accept << 1) | ((uint32_t)it.spp << 8);
         if (s < 2) state |= bits << (16 * s);
         else state_hi |= bits << (16 * (s - 2));
-        if (it.owner) {
-            st3(A.noisy_out, it.lin, it.color);
-            st_px(A.spp_out, it.lin, it.spp);
-            if constexpr (COH) st2_coh(coh_plane(A.prev_pixel_out), it.lin, make_float2(it.pfx, it.pfy));
-            else st_px(A.prev_pixel_out, it.lin, make_float2(it.pfx, it.pfy));
-        }
+        // owners only (bmfr.cl:478-484), as branch-free stores (st3_drop)
+        st3_drop(drop_plane(A.noisy_out), it.lin, it.owner, it.color);
+        st1_drop(drop_plane(A.spp_out), it.lin, it.owner, it.spp);
+        st2_drop<COH ? kSc1 : 0>(drop_plane(A.prev_pixel_out), it.lin, it.owner, make_float2(it.pfx, it.pfy));
     }
     report_reach(P, A.reach, over);
 

@@ -724,12 +724,10 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 L.keep_s[(i * 3 + 1) * NT + t] = it.prev_f.y;
                 L.keep_s[(i * 3 + 2) * NT + t] = it.prev_f.z;
             }
-            if (it.owner) {
-                st3(A.noisy_out, it.lin, it.color);
-                st_px(A.spp_out, it.lin, it.spp);
-                if constexpr (COH) st2_coh(coh_plane(A.prev_pixel_out), it.lin, make_float2(it.pfx, it.pfy));
-                else st_px(A.prev_pixel_out, it.lin, make_float2(it.pfx, it.pfy));
-            }
+            // owners only (bmfr.cl:478-484), as branch-free stores (st3_drop)
+            st3_drop(drop_plane(A.noisy_out), it.lin, it.owner, it.color);
+            st1_drop(drop_plane(A.spp_out), it.lin, it.owner, it.spp);
+            st2_drop<COH ? kSc1 : 0>(drop_plane(A.prev_pixel_out), it.lin, it.owner, make_float2(it.pfx, it.pfy));
             if (i & 1) {  // rows j = NI w + i - 1, NI w + i: adjacent halves of lane l's row slot
                 // (pair (NI w + i) / 2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)
                 const int pair = ((NI * w + i) / 2) ^ ((l >> 2) & 7);
@@ -782,6 +780,9 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
         wp[i] = widen(wp_r[i]);
     }
 
+#ifdef BMFR_PROBE_K1_NOP3  // timing probe (wrong results): no weighted sum / blend / stores
+    if (frame >= 0) return;
+#endif
     // ---- weighted_sum (bmfr.cl:717-750) + temporal blend (bmfr.cl:778-849) ----
     // Items (0, 1) and (2, 3) as packed f32 pairs: every lane rounds as
     // upstream's scalar sequence, each item in feature order.

@@ -273,9 +273,16 @@ __device__ __forceinline__ NoisyCur<IN> noisy_load_current(const Params& P, cons
     NoisyCur<IN> c;
     item_pixel(P, gx, gy, frame, c.px, c.py, c.owner);
     const uint32_t lin = pix(P, c.px, c.py);
+#ifdef BMFR_PROBE_K1_NOCUR  // timing probe (wrong results): current planes from one pixel (cache hits)
+    const uint32_t l0 = lin & 63u;
+    c.wp = ld3raw<IN>(in.p_cur, l0);
+    c.nrm = ld3raw<IN>(in.n_cur, l0);
+    if constexpr (COLOUR) c.cur = ld3raw<IN>(in.noisy_cur, l0);
+#else
     c.wp = ld3raw<IN>(in.p_cur, lin);
     c.nrm = ld3raw<IN>(in.n_cur, lin);
     if constexpr (COLOUR) c.cur = ld3raw<IN>(in.noisy_cur, lin);
+#endif
     return c;
 }
 
