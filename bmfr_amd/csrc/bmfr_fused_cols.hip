@@ -693,6 +693,12 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // out right behind item i's reprojection taps, so each wait for taps
     // leaves the next item's loads in flight.
     float kp[NI][3];  // keep_in_m(B): the kept colours, in registers until the fit has loaded M
+    // fast_fit at B = 13: phase 1's normal / position stay in registers for
+    // phase 3 (no second read of those planes: 24 B/px of f32 input; K1
+    // -4 %); the exact fit (K1 +12 %, 84-96 bytes of spills) and B = 16
+    // (76-144 bytes) hold too many registers for it.
+    constexpr bool kKeepNP = FAST && B < 16;
+    In3<IN> keep_n[NI], keep_p[NI];
     NoisyCur<IN> cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly, frame);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -701,6 +707,10 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
         if (i < NI - 1) nxt = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly + 2 * (i + 1), frame);
         __builtin_amdgcn_sched_barrier(0);
         const NoisyItem it = noisy_taps_finish<true, IN>(P, cur, tp, frame);
+        if constexpr (kKeepNP) {
+            keep_n[i] = cur.nrm;
+            keep_p[i] = cur.wp;
+        }
         {
 #pragma unroll
             for (int f = 1; f < B; ++f) {
@@ -760,8 +770,13 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
         const int px = bx * kEdge + (l3 & (kEdge - 1)) - kEdge / 2 + off.x;
         const int py = by * kEdge + (l3 >> 5) + 2 * NI * w + 2 * i - kEdge / 2 + off.y;
         lin[i] = pix(P, (ibits & (1u << i)) ? px : P.ox, (ibits & (1u << i)) ? py : P.oy);  // margins: a valid pixel, skipped below
-        nrm_r[i] = ld3raw<IN>(A.in.n_cur, lin[i]);
-        wp_r[i] = ld3raw<IN>(A.in.p_cur, lin[i]);
+        if constexpr (kKeepNP) {
+            nrm_r[i] = keep_n[i];
+            wp_r[i] = keep_p[i];
+        } else {
+            nrm_r[i] = ld3raw<IN>(A.in.n_cur, lin[i]);
+            wp_r[i] = ld3raw<IN>(A.in.p_cur, lin[i]);
+        }
     }
     k1_barrier();  // R complete (LDS); with LDS-only barriers the loads above stay in flight
     BMFR_STAMP(3);

@@ -788,21 +788,55 @@ __device__ __forceinline__ void taa_load_taps(const Params& P, float2 pf, const 
         pc[i] = ld3(prev_frame, pix(P, clamp_rx(P, ix + (i & 1)), clamp_ry(P, iy + (i >> 1))));
 }
 
-// TAA for one pixel (bmfr.cl:873-973) given its previous-frame taps (from
-// taa_load_taps) and the YCoCg of its 3x3 neighbourhood in the current
-// tone-mapped frame, nb[3 * (dy + 1) + (dx + 1)] (nb[4] is the centre's).
+// TAA for one pixel (bmfr.cl:873-973) in two halves.  taa_history: the
+// bilinear blend of the previous TAA output's taps (from taa_load_taps) at
+// reprojected position pf, in YCoCg (bmfr.cl:925-966); any value when the
+// reprojection is off-screen (taa_clamp then returns the pixel's own colour).
+// It needs no neighbour, so a tile forms it as soon as the taps arrive and
+// keeps three values instead of twelve.
+__device__ __forceinline__ f3 taa_history(const Params& P, float2 pf, const f3 (&pc)[4]) {
+    const int W = P.width, H = P.height;
+    const float flx = floorf(pf.x), fly = floorf(pf.y);
+    // as taa_load_taps: in the int range whatever pf is (the result is only
+    // used when pf is on screen, where this is the identity)
+    const int ix = (int)fminf(fmaxf(flx, -2.f), (float)W + 1.f);
+    const int iy = (int)fminf(fmaxf(fly, -2.f), (float)H + 1.f);
+    f3 prev{0.f, 0.f, 0.f};
+    float total = 0.f;
+    const float fx = pf.x - flx, fy = pf.y - fly;
+    const float omx = 1.f - fx, omy = 1.f - fy;
+    const float tw[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // bmfr.cl:929-960
+        const bool okx = (i & 1) ? (ix < W - 1) : (ix >= 0);
+        const bool oky = (i >> 1) ? (iy < H - 1) : (iy >= 0);
+        if (okx && oky) {
+            prev.x = prev.x + tw[i] * pc[i].x;
+            prev.y = prev.y + tw[i] * pc[i].y;
+            prev.z = prev.z + tw[i] * pc[i].z;
+            total = total + tw[i];
+        }
+    }
+    const float rt = 1.f / total;  // total can be 0 only in a degenerate case (bmfr.cl:962)
+    prev = f3{div_shared(prev.x, total, rt), div_shared(prev.y, total, rt), div_shared(prev.z, total, rt)};
+    return rgb_to_ycocg(prev);
+}
+
+// taa_clamp: the history py (taa_history) clamped to the YCoCg box / cross
+// of the pixel's 3x3 neighbourhood in the current tone-mapped frame,
+// nb[3 * (dy + 1) + (dx + 1)] (nb[4] is the centre's), and blended with the
+// pixel's own colour me.
 // CHECK: skip out-of-image neighbours as upstream does (any value may stand
 // in nb[] for them); without it every neighbour must be in the image.  A
 // skipped neighbour enters the min / max as +inf / -inf, which leaves them
 // unchanged bit for bit, so both forms are upstream's sequence.
 template <bool CHECK>
-__device__ __forceinline__ f3 taa_resolve(const Params& P, int x, int y, f3 me, float2 pf, const f3 (&nb)[9],
-                                          const f3 (&pc)[4], int frame) {
+__device__ __forceinline__ f3 taa_clamp(const Params& P, int x, int y, f3 me, float2 pf, const f3 (&nb)[9], f3 py,
+                                        int frame) {
     const int W = P.width, H = P.height;
     const float flx = floorf(pf.x), fly = floorf(pf.y);
     if (frame == 0 || flx < -1.f || fly < -1.f || flx >= (float)W || fly >= (float)H)
         return me;  // bmfr.cl:884-890 (compared as floats: no int overflow)
-    const int ix = (int)flx, iy = (int)fly;
     // bmfr.cl:897-920: min / max over the 3x3 box and the cross, visited dy
     // outer, dx inner.  A skipped neighbour enters as +inf / -inf; the
     // three-operand min / max keep upstream's left-to-right order exactly.
@@ -837,31 +871,19 @@ __device__ __forceinline__ f3 taa_resolve(const Params& P, int x, int y, f3 me, 
     box_cross([](const f3& v) { return v.x; }, mnb.x, mxb.x, mnc.x, mxc.x);
     box_cross([](const f3& v) { return v.y; }, mnb.y, mxb.y, mnc.y, mxc.y);
     box_cross([](const f3& v) { return v.z; }, mnb.z, mxb.z, mnc.z, mxc.z);
-    f3 prev{0.f, 0.f, 0.f};
-    float total = 0.f;
-    const float fx = pf.x - flx, fy = pf.y - fly;
-    const float omx = 1.f - fx, omy = 1.f - fy;
-    const float tw[4] = {omx * omy, fx * omy, omx * fy, fx * fy};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {  // bmfr.cl:929-960
-        const bool okx = (i & 1) ? (ix < W - 1) : (ix >= 0);
-        const bool oky = (i >> 1) ? (iy < H - 1) : (iy >= 0);
-        if (okx && oky) {
-            prev.x = prev.x + tw[i] * pc[i].x;
-            prev.y = prev.y + tw[i] * pc[i].y;
-            prev.z = prev.z + tw[i] * pc[i].z;
-            total = total + tw[i];
-        }
-    }
-    const float rt = 1.f / total;  // total can be 0 only in a degenerate case (bmfr.cl:962)
-    prev = f3{div_shared(prev.x, total, rt), div_shared(prev.y, total, rt), div_shared(prev.z, total, rt)};
-    const f3 py = rgb_to_ycocg(prev);
     const f3 lo{(mnb.x + mnc.x) / 2.f, (mnb.y + mnc.y) / 2.f, (mnb.z + mnc.z) / 2.f};
     const f3 hi{(mxb.x + mxc.x) / 2.f, (mxb.y + mxc.y) / 2.f, (mxb.z + mxc.z) / 2.f};
     const f3 cl{fminf(fmaxf(py.x, lo.x), hi.x), fminf(fmaxf(py.y, lo.y), hi.y), fminf(fmaxf(py.z, lo.z), hi.z)};
     const f3 pr = ycocg_to_rgb(cl);
     const float a = P.taa_blend_alpha, b = 1.f - a;
     return f3{a * me.x + b * pr.x, a * me.y + b * pr.y, a * me.z + b * pr.z};
+}
+
+// Both halves for one pixel.
+template <bool CHECK>
+__device__ __forceinline__ f3 taa_resolve(const Params& P, int x, int y, f3 me, float2 pf, const f3 (&nb)[9],
+                                          const f3 (&pc)[4], int frame) {
+    return taa_clamp<CHECK>(P, x, y, me, pf, nb, taa_history(P, pf, pc), frame);
 }
 
 }  // namespace bmfr

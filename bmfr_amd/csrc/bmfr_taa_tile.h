@@ -133,56 +133,98 @@ __device__ __forceinline__ void forward_reach(const TaaArgs& T, bool here = true
     }
 }
 
-// Y: (64 + 2) * (TH + 2) float4; sE / sRP: the powr tables' LDS copies.
-// COH: the tile runs in the launch that computes its K1 blocks: it waits for
-// them and reads their outputs with device-coherent loads.
-// NT threads (NT / 64 rows of 64 per pass).
-template <class IN, int TH, bool COH = false, int NT = 256>
-__device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int x0, int y0, float4* __restrict__ Y,
-                                         double* __restrict__ sE, double2* __restrict__ sRP) {
-    constexpr int RP = NT / 64;  // tile rows per pass
+// A tile's geometry: 64 x TH output pixels, NT threads (NT / 64 rows of 64
+// per pass, KN output pixels per thread), the tile and a 1-pixel ring in LDS.
+template <int TH, int NT>
+struct TileShape {
+    static constexpr int RP = NT / 64;  // tile rows per pass
     static_assert(TH % RP == 0 && TH >= RP, "tile height");
-    constexpr int HW = 64 + 2, HH = TH + 2, N = HW * HH;
-    constexpr int RING = N - 64 * TH;  // halo pixels
-    constexpr int KN = TH / RP;        // output pixels per thread
+    static constexpr int HW = 64 + 2, HH = TH + 2, N = HW * HH;
+    static constexpr int RING = N - 64 * TH;  // halo pixels
+    static constexpr int KN = TH / RP;        // output pixels per thread
     static_assert(RING <= NT, "one ring pixel per thread");
-    const int t = threadIdx.x;
-    bmfr_powr_tables_to_lds<NT>(sE, sRP, t);
-    const int tx = t & (64 - 1), ty = t >> 6;
-    if constexpr (COH) wait_k1_blocks(P, T, x0, y0, TH);
-    const CohPlane c_pp = coh_plane(T.prev_pixel), c_src = coh_plane(T.src);  // (unused unless COH)
-    // Reprojected positions first, then the tile and its ring behind them.
+};
+
+// A thread's current-frame inputs of one tile, as loaded: the reprojected
+// positions of its KN output pixels, and the colour and albedo of those and
+// of its ring pixel (k = KN, threads t < RING).
+template <class IN, int KN>
+struct TileLoads {
     float2 pf[KN];
-#pragma unroll
-    for (int k = 0; k < KN; ++k) {
-        const uint32_t i = pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + ty + RP * k, P.ty1 - 1));
-        if constexpr (COH) pf[k] = ld2_coh(c_pp, i);
-        else pf[k] = ld_px(T.prev_pixel, i);
-    }
     f3 v[KN + 1];
-    In3<IN> al[KN + 1];  // albedo as loaded, widened in the tone map (after the tap loads are out)
-    int hx = 0, hy = 0;  // this thread's ring pixel (t < RING), in tile + halo coordinates
-    if (t < 2 * HW) {
-        hx = t % HW;
-        hy = t < HW ? 0 : HH - 1;
+    In3<IN> al[KN + 1];  // widened in the tone map
+};
+
+// This thread's ring pixel (t < RING), in tile + halo coordinates.
+template <int TH, int NT>
+__device__ __forceinline__ void ring_pixel(int t, int& hx, int& hy) {
+    using S = TileShape<TH, NT>;
+    if (t < 2 * S::HW) {
+        hx = t % S::HW;
+        hy = t < S::HW ? 0 : S::HH - 1;
     } else {
-        hx = t < 2 * HW + TH ? 0 : HW - 1;
-        hy = 1 + (t - 2 * HW) % TH;
+        hx = t < 2 * S::HW + TH ? 0 : S::HW - 1;
+        hy = 1 + (t - 2 * S::HW) % TH;
+    }
+}
+
+// Issue the tile's current-frame loads (reprojected positions first).  COH:
+// device-coherent loads of K1's outputs of the same launch.
+template <class IN, int TH, bool COH, int NT>
+__device__ __forceinline__ void tile_issue(const Params& P, const TaaArgs& T, int x0, int y0, int hx, int hy,
+                                           TileLoads<IN, TileShape<TH, NT>::KN>& L) {
+    using S = TileShape<TH, NT>;
+    const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
+    const CohPlane c_pp = coh_plane(T.prev_pixel), c_src = coh_plane(T.src);  // (unused unless COH)
+#pragma unroll
+    for (int k = 0; k < S::KN; ++k) {
+        const uint32_t i = pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + ty + S::RP * k, P.ty1 - 1));
+        if constexpr (COH) L.pf[k] = ld2_coh(c_pp, i);
+        else L.pf[k] = ld_px(T.prev_pixel, i);
     }
 #pragma unroll
-    for (int k = 0; k <= KN; ++k) {
-        const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + RP * k + 1 : hy;
-        if (k == KN && t >= RING) break;
+    for (int k = 0; k <= S::KN; ++k) {
+        const int lx = k < S::KN ? tx + 1 : hx, ly = k < S::KN ? ty + S::RP * k + 1 : hy;
+        if (k == S::KN && t >= S::RING) break;
         // Clamped into the buffer region (= the image when untiled): a tile
         // whose last 64-px column or TH-row band overhangs its output reads
         // no pixel outside the region; such values reach no output pixel.
         const uint32_t lin = pix(P, clamp_rx(P, x0 - 1 + lx), clamp_ry(P, y0 - 1 + ly));
-        if constexpr (COH) v[k] = ld3_coh(c_src, lin);
-        else v[k] = ld3(T.src, lin);
-        al[k] = ld3raw<IN>(T.albedo, lin);
+        if constexpr (COH) L.v[k] = ld3_coh(c_src, lin);
+        else L.v[k] = ld3(T.src, lin);
+        L.al[k] = ld3raw<IN>(T.albedo, lin);
     }
-    // Previous-frame taps before the tone map: their latency hides under it.
-    f3 taps[KN][4];
+}
+
+// Tone map (bmfr.cl:851-856) of the loaded colours into the LDS window Y as
+// YCoCg; me[k]: this thread's own output pixels, tone-mapped RGB.
+template <class IN, int TH, int NT>
+__device__ __forceinline__ void tile_tone(const Params& P, const TileLoads<IN, TileShape<TH, NT>::KN>& L, int hx,
+                                          int hy, float4* __restrict__ Y, const double* __restrict__ sE,
+                                          const double2* __restrict__ sRP, f3 (&me)[TileShape<TH, NT>::KN]) {
+    using S = TileShape<TH, NT>;
+    const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
+#pragma unroll
+    for (int k = 0; k <= S::KN; ++k) {
+        if (k == S::KN && t >= S::RING) break;
+        const int lx = k < S::KN ? tx + 1 : hx, ly = k < S::KN ? ty + S::RP * k + 1 : hy;
+#ifdef BMFR_PROBE_K2_NOTONE  // timing probe (wrong results): no tone map
+        const f3 a = widen(L.al[k]);
+        const f3 v{L.v[k].x * a.x, L.v[k].y * a.y, L.v[k].z * a.z};
+#else
+        const f3 v = tone_map(P, widen(L.al[k]), L.v[k], sE, sRP);
+#endif
+        if (k < S::KN) me[k] = v;
+        const f3 yc = rgb_to_ycocg(v);
+        Y[ly * S::HW + lx] = make_float4(yc.x, yc.y, yc.z, 0.f);
+    }
+}
+
+// The previous TAA output's bilinear taps at each output pixel's reprojected
+// position (bmfr.cl:929-960).
+template <int KN>
+__device__ __forceinline__ void tile_taps(const Params& P, const TaaArgs& T, const float2 (&pf)[KN],
+                                          f3 (&taps)[KN][4]) {
 #pragma unroll
     for (int k = 0; k < KN; ++k) {
 #ifdef BMFR_PROBE_K2_NOTAPS  // timing probe (wrong results): no previous-frame taps
@@ -191,46 +233,74 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
         taa_load_taps(P, pf[k], T.prev_frame, taps[k]);
 #endif
     }
-    __syncthreads();  // the powr tables are in LDS
-#pragma unroll
-    for (int k = 0; k <= KN; ++k) {
-        if (k == KN && t >= RING) break;
-        const int lx = k < KN ? tx + 1 : hx, ly = k < KN ? ty + RP * k + 1 : hy;
-#ifdef BMFR_PROBE_K2_NOTONE  // timing probe (wrong results): no tone map
-        { const f3 a = widen(al[k]); v[k] = f3{v[k].x * a.x, v[k].y * a.y, v[k].z * a.z}; }
-#else
-        v[k] = tone_map(P, widen(al[k]), v[k], sE, sRP);
-#endif
-        const f3 yc = rgb_to_ycocg(v[k]);
-        Y[ly * HW + lx] = make_float4(yc.x, yc.y, yc.z, 0.f);
-    }
-    __syncthreads();
+}
+
+// The resolve of the tile's output pixels from the complete window Y
+// (bmfr.cl:897-973) and the stores.
+template <int TH, int NT>
+__device__ __forceinline__ void tile_resolve(const Params& P, const TaaArgs& T, int x0, int y0,
+                                             const float4* __restrict__ Y, const f3 (&me)[TileShape<TH, NT>::KN],
+                                             const float2 (&pf)[TileShape<TH, NT>::KN],
+                                             const f3 (&hist)[TileShape<TH, NT>::KN]) {
+    using S = TileShape<TH, NT>;
+    const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
     // Tiles that reach the image border check every neighbour (bmfr.cl:901);
     // the others have all nine in the image.
     const bool edge = x0 == 0 || y0 == 0 || x0 + 64 >= P.width || y0 + TH >= P.height;
 #pragma unroll
-    for (int k = 0; k < KN; ++k) {
-        const int x = x0 + tx, y = y0 + ty + RP * k;
+    for (int k = 0; k < S::KN; ++k) {
+        const int x = x0 + tx, y = y0 + ty + S::RP * k;
         if (x < P.tx1 && y < P.ty1) {
-            const int c = (ty + RP * k + 1) * HW + tx + 1;
+            const int c = (ty + S::RP * k + 1) * S::HW + tx + 1;
             f3 nb[9];
 #pragma unroll
             for (int j = 0; j < 9; ++j) {
-                const float4 q = Y[c + (j / 3 - 1) * HW + (j % 3 - 1)];
+                const float4 q = Y[c + (j / 3 - 1) * S::HW + (j % 3 - 1)];
                 nb[j] = f3{q.x, q.y, q.z};
             }
 #ifdef BMFR_PROBE_K2_NORESOLVE  // timing probe (wrong results): no TAA resolve
-            f3 r = v[k];
+            f3 r = me[k];
 #pragma unroll
             for (int j = 0; j < 9; ++j) r = f3{r.x + nb[j].x, r.y + nb[j].y, r.z + nb[j].z};
-            r = f3{r.x + taps[k][0].x + taps[k][3].y, r.y, r.z};
+            r = f3{r.x + hist[k].x, r.y + hist[k].y, r.z + hist[k].z};
 #else
-            const f3 r = edge ? taa_resolve<true>(P, x, y, v[k], pf[k], nb, taps[k], T.frame)
-                              : taa_resolve<false>(P, x, y, v[k], pf[k], nb, taps[k], T.frame);
+            const f3 r = edge ? taa_clamp<true>(P, x, y, me[k], pf[k], nb, hist[k], T.frame)
+                              : taa_clamp<false>(P, x, y, me[k], pf[k], nb, hist[k], T.frame);
 #endif
             st3(T.result, pix(P, x, y), r);
         }
     }
+}
+
+// One tile.  Y: (64 + 2) * (TH + 2) float4; sE / sRP: the powr tables' LDS
+// copies.  COH: the tile runs in the launch that computes its K1 blocks: it
+// waits for them and reads their outputs with device-coherent loads.
+// Order: current-frame loads, tone map into LDS, then the previous-frame
+// taps (their latency under the barrier), each pixel's history as its taps
+// arrive (three values live instead of twelve: 89 VGPRs, five waves per
+// SIMD, where taps issued before the tone map held 124), the resolve.
+template <class IN, int TH, bool COH = false, int NT = 256>
+__device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int x0, int y0, float4* __restrict__ Y,
+                                         double* __restrict__ sE, double2* __restrict__ sRP) {
+    using S = TileShape<TH, NT>;
+    constexpr int KN = S::KN;
+    const int t = threadIdx.x;
+    bmfr_powr_tables_to_lds<NT>(sE, sRP, t);
+    if constexpr (COH) wait_k1_blocks(P, T, x0, y0, TH);
+    int hx = 0, hy = 0;
+    ring_pixel<TH, NT>(t, hx, hy);
+    TileLoads<IN, KN> L;
+    tile_issue<IN, TH, COH, NT>(P, T, x0, y0, hx, hy, L);
+    __syncthreads();  // the powr tables are in LDS
+    f3 me[KN];
+    tile_tone<IN, TH, NT>(P, L, hx, hy, Y, sE, sRP, me);
+    f3 taps[KN][4];
+    tile_taps<KN>(P, T, L.pf, taps);
+    __syncthreads();  // the window is complete
+    f3 hist[KN];
+#pragma unroll
+    for (int k = 0; k < KN; ++k) hist[k] = taa_history(P, L.pf[k], taps[k]);
+    tile_resolve<TH, NT>(P, T, x0, y0, Y, me, L.pf, hist);
 }
 
 // The TAA part of a one-launch frame kernel (K1 blocks, then the frame's
