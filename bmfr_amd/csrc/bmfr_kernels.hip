@@ -117,8 +117,13 @@ constexpr int kTaaW = 64, kTaaH = 12;
 #define BMFR_K2_NT 256
 #endif
 constexpr int kTaaNT = BMFR_K2_NT;
+// Minimum waves per SIMD for the register allocator (experiment knob; the
+// default leaves it free: 90 VGPRs, five waves).
+#ifndef BMFR_K2_MINW
+#define BMFR_K2_MINW 1
+#endif
 template <class IN>
-__global__ __launch_bounds__(kTaaNT) void k_fused_taa(Params P, TaaArgs T) {
+__global__ __launch_bounds__(kTaaNT, BMFR_K2_MINW) void k_fused_taa(Params P, TaaArgs T) {
     __shared__ float4 Y[(kTaaW + 2) * (kTaaH + 2)];  // YCoCg (+ pad): one 16-byte read per neighbour
     __shared__ double sE[kPowrENum];
     __shared__ double2 sRP[kPowrRPNum];
@@ -282,7 +287,9 @@ hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A) 
 hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& A, hipEvent_t mid) {
     hipError_t e;
     // One launch for the frame, unless K1 and K2 are timed apart (mid event).
+#ifndef BMFR_FRAME_TWO_LAUNCH
     if (!mid && A.done && frame_fused_supported(P)) return launch_fused_frame_one(P, st, A);
+#endif
     if (fused_supported(P)) {
         if ((e = launch_fused_k1_blocks(P, st, A)) != hipSuccess) return e;
         if (mid) (void)hipEventRecord(mid, st);

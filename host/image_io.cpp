@@ -1,4 +1,4 @@
-// image_io.cpp -- OpenEXR (scanline and tiled, NONE/RLE/ZIPS/ZIP/PIZ/PXR24/B44/B44A) and
+// image_io.cpp -- OpenEXR (scanline and tiled, NONE/RLE/ZIPS/ZIP/PIZ/PXR24/B44/B44A/DWAA/DWAB) and
 // PNG I/O over zlib.  See image_io.h.  The EXR layout follows the published
 // OpenEXR 2 file format: magic + version, attribute list, per-chunk offset
 // table, chunks of (y, size, data) -- tiled files: (tile x, tile y, level x,
@@ -9,6 +9,8 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <array>
+#include <cctype>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -54,8 +56,9 @@ int lines_per_chunk(int compression) {
     switch (compression) {
         case BMFR_EXR_NONE: case BMFR_EXR_RLE: case BMFR_EXR_ZIPS: return 1;
         case BMFR_EXR_ZIP: case BMFR_EXR_PXR24: return 16;
-        case BMFR_EXR_PIZ: case BMFR_EXR_B44: case BMFR_EXR_B44A: return 32;
-        default: return 0;  // DWAA/B (8, 9): unsupported
+        case BMFR_EXR_PIZ: case BMFR_EXR_B44: case BMFR_EXR_B44A: case BMFR_EXR_DWAA: return 32;
+        case BMFR_EXR_DWAB: return 256;
+        default: return 0;
     }
 }
 
@@ -184,6 +187,25 @@ float half_to_float(uint16_t h) {
     float f;
     std::memcpy(&f, &bits, 4);
     return f;
+}
+
+// float -> half, rounded to nearest even (overflow -> inf, NaN kept quiet).
+uint16_t float_to_half(float f) {
+    uint32_t x;
+    std::memcpy(&x, &f, 4);
+    const uint16_t s = (uint16_t)((x >> 16) & 0x8000);
+    const uint32_t a = x & 0x7fffffffu;
+    if (a >= 0x7f800000u) return (uint16_t)(s | 0x7c00 | (a > 0x7f800000u ? 0x200 : 0));
+    if (a >= 0x477ff000u) return (uint16_t)(s | 0x7c00);  // rounds past 65504
+    if (a < 0x38800000u) {  // half subnormal (or zero)
+        if (a < 0x33000000u) return s;  // below half the smallest subnormal: +-0
+        const uint32_t e = a >> 23, m = (a & 0x7fffff) | 0x800000;
+        const int shift = 126 - (int)e;  // 14 .. 24: value = m * 2^(e - 150), subnormal unit 2^-24
+        const uint32_t q = m >> shift, r = m & ((1u << shift) - 1), half_ = 1u << (shift - 1);
+        return (uint16_t)(s | (q + (r > half_ || (r == half_ && (q & 1)))));
+    }
+    const uint32_t q = (a - 0x38000000u) >> 13, r = a & 0x1fff;
+    return (uint16_t)(s | (q + (r > 0x1000 || (r == 0x1000 && (q & 1)))));
 }
 
 // Undo ZIP/RLE preprocessing: delta predictor, then de-interleave the two halves.
@@ -678,6 +700,358 @@ bool uncompress(const ExrHeader& h, const uint8_t* in, size_t n, int width, int 
 
 }  // namespace b44
 
+// ------------------------------------------------------------------ DWA --
+// The published OpenEXR DWAA / DWAB scheme (DreamWorks' lossy DCT codec),
+// decoder side.  A chunk (32 lines DWAA, 256 DWAB) is
+//   11 little-endian u64: version, unknown uncompressed / compressed size,
+//     AC compressed size, DC compressed size, RLE compressed / uncompressed /
+//     raw size, AC and DC value counts, AC compression (0 static Huffman --
+//     PIZ's coder --, 1 deflate);
+//   version 2: the channel rules, a u16 byte count (itself included) and
+//     rules of (channel-name suffix, a byte (CSC index + 1) << 4 | scheme << 2
+//     | case-insensitive, a pixel type); version 1 uses the fixed legacy set;
+//   then the UNKNOWN, AC, DC and RLE sections.
+// Each channel takes the scheme of the first rule matching its name's last
+// '.'-component and its type (none: UNKNOWN).
+//   UNKNOWN: the channels' raw lines (each line: those channels in order),
+//     zlib-compressed.
+//   RLE: per channel, its samples' bytes as byte planes (plane k: byte k of
+//     every sample, rows in order), the channels one after another, then
+//     OpenEXR RLE, then zlib.
+//   LOSSY_DCT (HALF only): 8 x 8 blocks, rows of blocks top to bottom; each
+//     block's 64 DCT coefficients are halves in zig-zag order -- the DC term
+//     in the DC section (per decoded channel, all its blocks; zlib with
+//     ZIP's byte predictor and interleave), the 63 AC terms in the AC section,
+//     block after block (per block, each channel of a colour set in turn):
+//     0xff00 ends the block (the rest zero), 0xffnn skips nn zeros, any other
+//     word is the next coefficient.  The decoder forms the inverse DCT
+//     (x = sum_k c_k / 2 X_k cos((2n + 1) k pi / 16), c_0 = 1/sqrt 2, rows then
+//     columns) in float, for an R, G, B set (CSC indices 0, 1, 2 under one
+//     prefix) converts Y'CbCr to RGB (BT.709: R = Y + 1.5747 Cr, G = Y -
+//     0.1873 Cb - 0.4682 Cr, B = Y + 1.8556 Cb), rounds each value to half
+//     and maps it from the codec's perceptual scale to linear (table below:
+//     |y|^2.2 up to 1, exp(2.2 (|y| - 1)) above, sign kept; non-finite -> 0).
+//     Decoded channels come in this order: the colour sets, then the other
+//     LOSSY_DCT channels, in channel-list order.
+// Parity is unpinned: no OpenEXR library and no reference DWA file exist
+// here; tests/exr_dwa_py.py is an independent encoder of the same scheme.
+namespace dwa {
+
+enum Scheme { kUnknown = 0, kLossyDct = 1, kRle = 2 };
+
+struct Rule {
+    std::string suffix;
+    int csc;  // -1, or the colour index 0 / 1 / 2 (R / G / B)
+    int scheme;
+    bool nocase;
+    int type;
+};
+
+const std::vector<Rule>& legacy_rules() {
+    static const std::vector<Rule> r = {
+        {"r", 0, kLossyDct, true, kHalf},     {"red", 0, kLossyDct, true, kHalf},
+        {"g", 1, kLossyDct, true, kHalf},     {"grn", 1, kLossyDct, true, kHalf},
+        {"green", 1, kLossyDct, true, kHalf}, {"b", 2, kLossyDct, true, kHalf},
+        {"blu", 2, kLossyDct, true, kHalf},   {"blue", 2, kLossyDct, true, kHalf},
+        {"y", -1, kLossyDct, true, kHalf},    {"by", -1, kLossyDct, true, kHalf},
+        {"ry", -1, kLossyDct, true, kHalf},   {"a", -1, kRle, true, kUint},
+        {"a", -1, kRle, true, kHalf},         {"a", -1, kRle, true, kFloat},
+    };
+    return r;
+}
+
+std::string lower(std::string s) {
+    for (char& ch : s) ch = (char)std::tolower((unsigned char)ch);
+    return s;
+}
+
+// The channel's rule: scheme and CSC index.
+void classify(const std::vector<Rule>& rules, const Channel& c, int& scheme, int& csc) {
+    const size_t dot = c.name.rfind('.');
+    const std::string suffix = dot == std::string::npos ? c.name : c.name.substr(dot + 1);
+    for (const Rule& r : rules) {
+        if (r.type != c.type) continue;
+        if (r.nocase ? lower(suffix) == lower(r.suffix) : suffix == r.suffix) {
+            scheme = r.scheme;
+            csc = r.csc;
+            return;
+        }
+    }
+    scheme = kUnknown;
+    csc = -1;
+}
+
+// Perceptual half -> linear half (the codec's inverse transfer).
+const std::vector<uint16_t>& to_linear() {
+    static const std::vector<uint16_t> t = [] {
+        std::vector<uint16_t> v(1 << 16);
+        for (uint32_t b = 0; b < (1u << 16); ++b) {
+            const float f = half_to_float((uint16_t)b);
+            double lin = 0.0;
+            if (std::isfinite(f)) {
+                const double a = std::fabs((double)f);
+                lin = a <= 1.0 ? std::pow(a, 2.2) : std::exp(2.2 * (a - 1.0));
+                if (f < 0) lin = -lin;
+            }
+            v[b] = float_to_half((float)lin);
+        }
+        return v;
+    }();
+    return t;
+}
+
+constexpr int kZigZag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                             12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                             35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                             58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// In-place 8 x 8 inverse DCT (rows, then columns), float.
+void idct8x8(float (&b)[64]) {
+    static const std::vector<float> T = [] {
+        std::vector<float> m(64);
+        const double pi = 3.14159265358979323846;
+        for (int k = 0; k < 8; ++k)
+            for (int n = 0; n < 8; ++n)
+                m[k * 8 + n] = (float)((k == 0 ? std::sqrt(0.5) : 1.0) * 0.5 * std::cos((2 * n + 1) * k * pi / 16));
+        return m;
+    }();
+    float t[64];
+    for (int r = 0; r < 8; ++r)
+        for (int n = 0; n < 8; ++n) {
+            float s = 0.f;
+            for (int k = 0; k < 8; ++k) s += T[k * 8 + n] * b[r * 8 + k];
+            t[r * 8 + n] = s;
+        }
+    for (int c = 0; c < 8; ++c)
+        for (int n = 0; n < 8; ++n) {
+            float s = 0.f;
+            for (int k = 0; k < 8; ++k) s += T[k * 8 + n] * t[k * 8 + c];
+            b[n * 8 + c] = s;
+        }
+}
+
+uint64_t rd64(const uint8_t* p) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    return v;
+}
+
+// zlib into exactly `want` bytes.
+bool inflate_exact(const uint8_t* in, uint64_t n, std::vector<uint8_t>& out, uint64_t want) {
+    if (want > (1ull << 31) || n > (1ull << 31)) return false;
+    out.resize((size_t)want);
+    if (want == 0) return n == 0;
+    uLongf got = (uLongf)want;
+    return uncompress(out.data(), &got, in, (uLong)n) == Z_OK && got == want;
+}
+
+bool uncompress(const ExrHeader& h, const uint8_t* in, size_t n, int width, int lines, std::vector<uint8_t>& raw) {
+    constexpr int kSizes = 11;
+    if (n < 8 * kSizes) return false;
+    uint64_t sz[kSizes];
+    for (int i = 0; i < kSizes; ++i) sz[i] = rd64(in + 8 * i);
+    const uint64_t version = sz[0], unk_raw = sz[1], unk_comp = sz[2], ac_comp = sz[3], dc_comp = sz[4],
+                   rle_comp = sz[5], rle_unc = sz[6], rle_raw = sz[7], ac_count = sz[8], dc_count = sz[9],
+                   ac_mode = sz[10];
+    if (version > 2 || ac_mode > 1) return false;
+    const uint8_t* p = in + 8 * kSizes;
+    const uint8_t* const end = in + n;
+    std::vector<Rule> rules;
+    if (version == 2) {
+        if (end - p < 2) return false;
+        const uint16_t rule_bytes = (uint16_t)(p[0] | p[1] << 8);
+        if (rule_bytes < 2 || rule_bytes > end - p) return false;
+        const uint8_t* r = p + 2;
+        const uint8_t* const rend = p + rule_bytes;
+        while (r < rend) {
+            const uint8_t* z = (const uint8_t*)std::memchr(r, 0, (size_t)(rend - r));
+            if (!z || rend - z < 3) return false;
+            Rule ru;
+            ru.suffix.assign((const char*)r, (size_t)(z - r));
+            const uint8_t v = z[1];
+            ru.csc = (v >> 4) - 1;
+            ru.scheme = (v >> 2) & 3;
+            ru.nocase = (v & 1) != 0;
+            ru.type = z[2];
+            if (ru.csc > 2 || ru.scheme > kRle || ru.type > kFloat) return false;
+            rules.push_back(ru);
+            r = z + 3;
+        }
+        p = rend;
+    } else {
+        rules = legacy_rules();
+    }
+    // the sections, in order, inside the chunk
+    const uint64_t left = (uint64_t)(end - p);
+    if (unk_comp > left || ac_comp > left - unk_comp || dc_comp > left - unk_comp - ac_comp ||
+        rle_comp > left - unk_comp - ac_comp - dc_comp)
+        return false;
+    const uint8_t* unk_p = p;
+    const uint8_t* ac_p = unk_p + unk_comp;
+    const uint8_t* dc_p = ac_p + ac_comp;
+    const uint8_t* rle_p = dc_p + dc_comp;
+
+    // channel schemes and colour sets
+    const size_t nc = h.channels.size();
+    std::vector<int> scheme(nc), csc(nc);
+    for (size_t i = 0; i < nc; ++i) classify(rules, h.channels[i], scheme[i], csc[i]);
+    std::vector<std::array<int, 3>> sets;  // channel indices of complete R, G, B sets
+    std::vector<int> in_set(nc, 0);
+    {
+        std::vector<std::string> prefix(nc);
+        for (size_t i = 0; i < nc; ++i) {
+            const size_t dot = h.channels[i].name.rfind('.');
+            prefix[i] = dot == std::string::npos ? std::string() : h.channels[i].name.substr(0, dot + 1);
+        }
+        std::vector<int> used(nc, 0);
+        for (size_t i = 0; i < nc; ++i) {
+            if (scheme[i] != kLossyDct || csc[i] < 0 || used[i]) continue;
+            std::array<int, 3> s = {-1, -1, -1};
+            for (size_t j = 0; j < nc; ++j)
+                if (scheme[j] == kLossyDct && csc[j] >= 0 && !used[j] && prefix[j] == prefix[i] && s[csc[j]] < 0)
+                    s[csc[j]] = (int)j;
+            if (s[0] >= 0 && s[1] >= 0 && s[2] >= 0) {
+                for (int k : s) used[k] = in_set[k] = 1;
+                sets.push_back(s);
+            }
+        }
+    }
+    for (size_t i = 0; i < nc; ++i)
+        if (scheme[i] == kLossyDct && h.channels[i].type != kHalf) return false;
+
+    // per-channel decoded planes (row-major, type_bytes per sample)
+    std::vector<std::vector<uint8_t>> plane(nc);
+    const size_t W = (size_t)width, L = (size_t)lines;
+
+    // UNKNOWN
+    {
+        size_t line_bytes = 0;
+        for (size_t i = 0; i < nc; ++i)
+            if (scheme[i] == kUnknown) line_bytes += W * type_bytes(h.channels[i].type);
+        if (unk_raw != line_bytes * L) return false;
+        std::vector<uint8_t> u;
+        if (!inflate_exact(unk_p, unk_comp, u, unk_raw)) return false;
+        size_t o = 0;
+        for (size_t y = 0; y < L; ++y)
+            for (size_t i = 0; i < nc; ++i) {
+                if (scheme[i] != kUnknown) continue;
+                const size_t row = W * type_bytes(h.channels[i].type);
+                plane[i].resize(row * L);
+                std::memcpy(plane[i].data() + y * row, u.data() + o, row);
+                o += row;
+            }
+    }
+    // RLE
+    {
+        size_t want = 0;
+        for (size_t i = 0; i < nc; ++i)
+            if (scheme[i] == kRle) want += W * L * type_bytes(h.channels[i].type);
+        if (rle_raw != want) return false;
+        std::vector<uint8_t> r;
+        if (want > 0) {
+            std::vector<uint8_t> z;
+            if (!inflate_exact(rle_p, rle_comp, z, rle_unc)) return false;
+            if (!rle_decode(z.data(), z.size(), r, want)) return false;
+        } else if (rle_comp != 0 || rle_unc != 0) {
+            return false;
+        }
+        size_t o = 0;
+        for (size_t i = 0; i < nc; ++i) {
+            if (scheme[i] != kRle) continue;
+            const int tb = type_bytes(h.channels[i].type);
+            plane[i].resize(W * L * tb);
+            for (int k = 0; k < tb; ++k)
+                for (size_t s = 0; s < W * L; ++s) plane[i][s * tb + k] = r[o + k * W * L + s];
+            o += W * L * tb;
+        }
+    }
+    // LOSSY_DCT
+    const size_t bx = (W + 7) / 8, by = (L + 7) / 8, nb = bx * by;
+    size_t n_dct = 0;
+    for (size_t i = 0; i < nc; ++i) n_dct += scheme[i] == kLossyDct;
+    if (dc_count != nb * n_dct || ac_count > (uint64_t)63 * nb * n_dct) return false;
+    std::vector<uint16_t> ac((size_t)ac_count), dc((size_t)dc_count);
+    if (n_dct > 0) {
+        if (ac_mode == 0) {
+            if (!piz::huf_uncompress(ac_p, (size_t)ac_comp, ac.data(), ac.size())) return false;
+        } else {
+            std::vector<uint8_t> t;
+            if (!inflate_exact(ac_p, ac_comp, t, 2 * ac_count)) return false;
+            std::memcpy(ac.data(), t.data(), t.size());
+        }
+        std::vector<uint8_t> t;
+        if (!inflate_exact(dc_p, dc_comp, t, 2 * dc_count)) return false;
+        std::vector<uint8_t> d(t.size());
+        if (!t.empty()) unpredict_deinterleave(t, d.data());
+        std::memcpy(dc.data(), d.data(), d.size());
+    } else if (ac_count || dc_count || ac_comp || dc_comp) {
+        return false;
+    }
+    // decoders: the colour sets, then the other lossy channels
+    std::vector<std::vector<int>> decoders;
+    for (const auto& s : sets) decoders.push_back({s[0], s[1], s[2]});
+    for (size_t i = 0; i < nc; ++i)
+        if (scheme[i] == kLossyDct && !in_set[i]) decoders.push_back({(int)i});
+    const std::vector<uint16_t>& lin = to_linear();
+    size_t ai = 0, di = 0;
+    for (const auto& dec : decoders) {
+        const size_t k = dec.size();
+        for (int c : dec) plane[c].assign(W * L * 2, 0);
+        for (size_t b = 0; b < nb; ++b) {
+            float blk[3][64];
+            for (size_t c = 0; c < k; ++c) {
+                uint16_t z[64] = {};
+                z[0] = dc[di + c * nb + b];
+                int pos = 1;
+                while (pos < 64) {
+                    if (ai >= ac.size()) return false;
+                    const uint16_t v = ac[ai++];
+                    if (v == 0xff00) {
+                        pos = 64;
+                    } else if ((v >> 8) == 0xff) {
+                        pos += v & 0xff;
+                        if (pos > 64) return false;
+                    } else {
+                        z[pos++] = v;
+                    }
+                }
+                for (int j = 0; j < 64; ++j) blk[c][kZigZag[j]] = half_to_float(z[j]);
+                idct8x8(blk[c]);
+            }
+            if (k == 3) {
+                for (int j = 0; j < 64; ++j) {
+                    const float y = blk[0][j], cb = blk[1][j], cr = blk[2][j];
+                    blk[0][j] = y + 1.5747f * cr;
+                    blk[1][j] = y - 0.1873f * cb - 0.4682f * cr;
+                    blk[2][j] = y + 1.8556f * cb;
+                }
+            }
+            const size_t x0 = (b % bx) * 8, y0 = (b / bx) * 8;
+            for (size_t c = 0; c < k; ++c)
+                for (size_t dy = 0; dy < 8 && y0 + dy < L; ++dy)
+                    for (size_t dx = 0; dx < 8 && x0 + dx < W; ++dx) {
+                        const uint16_t v = lin[float_to_half(blk[c][dy * 8 + dx])];
+                        uint8_t* o = plane[dec[c]].data() + ((y0 + dy) * W + x0 + dx) * 2;
+                        o[0] = (uint8_t)(v & 0xff);
+                        o[1] = (uint8_t)(v >> 8);
+                    }
+        }
+        di += k * nb;
+    }
+    if (ai != ac.size()) return false;
+    // interleave per line, channel-list order
+    uint8_t* o = raw.data();
+    for (size_t y = 0; y < L; ++y)
+        for (size_t i = 0; i < nc; ++i) {
+            const size_t row = W * type_bytes(h.channels[i].type);
+            std::memcpy(o, plane[i].data() + y * row, row);
+            o += row;
+        }
+    return true;
+}
+
+}  // namespace dwa
+
 // One chunk (scanline block, or tile) of `lines` lines x `width` pixels.
 bool decode_chunk(const ExrHeader& h, const uint8_t* data, size_t size, size_t raw_size, int width, int lines,
                   std::vector<uint8_t>& raw) {
@@ -696,6 +1070,8 @@ bool decode_chunk(const ExrHeader& h, const uint8_t* data, size_t size, size_t r
     if (compression == BMFR_EXR_PXR24) return pxr24_uncompress(h, data, size, width, lines, raw);
     if (compression == BMFR_EXR_B44 || compression == BMFR_EXR_B44A)
         return b44::uncompress(h, data, size, width, lines, raw);
+    if (compression == BMFR_EXR_DWAA || compression == BMFR_EXR_DWAB)
+        return dwa::uncompress(h, data, size, width, lines, raw);
     std::vector<uint8_t> t;
     if (compression == BMFR_EXR_RLE) {
         if (!rle_decode(data, size, t, raw_size)) return false;

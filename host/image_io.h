@@ -5,10 +5,12 @@
  * channels) and the PNG output of bmfr.cpp:519-553 (ImageOutput, FLOAT ->
  * 8 bit).  Self-contained over zlib: OpenEXR 2.x single-part files, scanline
  * or tiled (one-level; the full-resolution level of mip / rip maps), with
- * HALF / FLOAT / UINT channels and NONE, RLE, ZIPS, ZIP, PIZ, PXR24, B44 or
- * B44A compression (the formats of the BMFR dataset and of common renderers;
- * DWAA / DWAB, B44 channels with the pLinear flag and deep / multi-part files
- * are rejected with an error); writer: FLOAT RGB, NONE or ZIP.
+ * HALF / FLOAT / UINT channels and NONE, RLE, ZIPS, ZIP, PIZ, PXR24, B44,
+ * B44A, DWAA or DWAB compression (the formats of the BMFR dataset and of
+ * common renderers; B44 channels with the pLinear flag and deep / multi-part
+ * files are rejected with an error); writer: FLOAT RGB, NONE or ZIP.  No
+ * OpenEXR library or reference file exists here: parity is unpinned (the
+ * tests check against independent encoders of the published schemes).
  */
 #ifndef BMFR_IMAGE_IO_H
 #define BMFR_IMAGE_IO_H
@@ -27,7 +29,9 @@ typedef enum bmfr_exr_compression {
     BMFR_EXR_PIZ = 4,   /* read only */
     BMFR_EXR_PXR24 = 5, /* read only (lossy: FLOAT samples keep 24 bits) */
     BMFR_EXR_B44 = 6,   /* read only (lossy for HALF samples: 4x4 blocks in 14 bytes) */
-    BMFR_EXR_B44A = 7   /* read only (B44, flat blocks in 3 bytes) */
+    BMFR_EXR_B44A = 7,  /* read only (B44, flat blocks in 3 bytes) */
+    BMFR_EXR_DWAA = 8,  /* read only (lossy DCT of HALF colour channels, 32 lines per chunk) */
+    BMFR_EXR_DWAB = 9   /* read only (DWAA with 256 lines per chunk) */
 } bmfr_exr_compression;
 
 /* Size of an EXR file's data window.  0 on success, else -1 (message via

@@ -1,8 +1,9 @@
 """EXR / PNG I/O of the host (host/image_io.cpp), checked
 against an independent numpy + zlib implementation of the same published
 formats written here: OpenEXR 2 scanline and tiled files (HALF / FLOAT
-channels, NONE / RLE / ZIPS / ZIP / PXR24 compression, and PIZ through the
-independent encoder tests/exr_piz_py.py; one-level and mip-mapped tiles) and
+channels, NONE / RLE / ZIPS / ZIP / PXR24 / B44 / B44A compression, PIZ
+through the independent encoder tests/exr_piz_py.py and DWAA / DWAB through
+tests/exr_dwa_py.py; one-level and mip-mapped tiles) and
 8-bit RGB PNG.  EXR parity is unpinned: no OpenEXR library and no reference
 .exr file exist here, so the reader is only as right as these encoders'
 reading of the published format."""
@@ -17,6 +18,7 @@ import numpy as np
 import pytest
 
 from bmfr_amd import _build
+import exr_dwa_py
 import exr_piz_py
 from exr_piz_py import piz_compress
 
@@ -181,6 +183,8 @@ def _b44(img, names, y0, lines, x0, w, half, flat, types):
 
 
 RAW_CHUNKS = []  # (level, y0, lines, x0, w) of the chunks write_exr_py stored uncompressed
+DWA_DECODED = {}  # channel -> {(y0, x0): the chunk's samples as a DWA decoder produces them}
+DWA_OPTS = {"version": 2, "ac_mode": 0, "drop": 0.02}  # DWA chunks' form (exr_dwa_py.dwa_compress)
 
 
 def _chunk_data(img, names, dt, compression, y0, lines, x0, w, half, level=0, types=None):
@@ -198,6 +202,12 @@ def _chunk_data(img, names, dt, compression, y0, lines, x0, w, half, level=0, ty
         data = _pxr24(img, names, y0, lines, x0, w, half)
     elif compression in (6, 7):
         data = _b44(img, names, y0, lines, x0, w, half, compression == 7, types)
+    elif compression in (8, 9):
+        ptypes = {n: (1 if types.get(n, half) else 2) for n in names}
+        data, dec = exr_dwa_py.dwa_compress({n: img[n][y0:y0 + lines, x0:x0 + w] for n in names}, ptypes, lines, w,
+                                            **DWA_OPTS)
+        for n in names:
+            DWA_DECODED.setdefault(n, {})[(y0, x0)] = dec[n]
     else:
         data = raw
     if compression and len(data) >= len(raw):  # OpenEXR stores such a chunk as it is
@@ -209,8 +219,8 @@ def _chunk_data(img, names, dt, compression, y0, lines, x0, w, half, level=0, ty
 def write_exr_py(path, img: dict, compression: int, half: bool, tile=None, mipmap=False, types=None):
     """img: channel name -> (H, W) float array.  Channels are stored sorted by
     name.  compression 0 NONE, 1 RLE, 2 ZIPS, 3 ZIP, 4 PIZ, 5 PXR24, 6 B44,
-    7 B44A.  types: channel name -> True (HALF) / False (FLOAT) where it
-    differs from `half` (B44 chunks only).
+    7 B44A, 8 DWAA, 9 DWAB.  types: channel name -> True (HALF) / False
+    (FLOAT) where it differs from `half` (B44 / DWA chunks only).
     tile = (tw, th): a tiled file (ONE_LEVEL, or MIPMAP_LEVELS round-down
     with mipmap=True: the lower levels follow level 0, box-filtered)."""
     names = sorted(img)
@@ -246,7 +256,7 @@ def write_exr_py(path, img: dict, compression: int, half: bool, tile=None, mipma
                     data = _chunk_data(im, names, dt, compression, y0, lines, x0, w, half, lv, types)
                     chunks.append(struct.pack("<iiiii", tx, ty, lv, lv, len(data)) + data)
     else:
-        lpc = {0: 1, 1: 1, 2: 1, 3: 16, 4: 32, 5: 16, 6: 32, 7: 32}[compression]
+        lpc = {0: 1, 1: 1, 2: 1, 3: 16, 4: 32, 5: 16, 6: 32, 7: 32, 8: 32, 9: 256}[compression]
         for y0 in range(0, H, lpc):
             data = _chunk_data(img, names, dt, compression, y0, min(H, y0 + lpc) - y0, 0, W, half, types=types)
             chunks.append(struct.pack("<ii", y0, len(data)) + data)
@@ -549,3 +559,113 @@ def test_exr_b44_rejects_plinear(tmp_path):
     out = np.empty_like(img)
     assert lib().bmfr_exr_read_rgb(str(path).encode(), 8, 8, out.ctypes.data) != 0
     assert b"pLinear" in lib().bmfr_io_error()
+
+
+def _dwa_image(H, W, seed):
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    r = 0.5 + 0.4 * np.sin(xx / 7.0) * np.cos(yy / 5.0)                       # smooth, below 1
+    g = np.abs(0.3 + 0.1 * np.sin(yy / 3.0) + rng.normal(0, 0.03, (H, W))).astype(np.float32)  # noise
+    b = (1.0 + 30.0 * (xx + yy) / (W + H)).astype(np.float32)                 # above 1: the log branch
+    b[::5, ::3] *= -1.0                                                      # negative samples
+    g[0, 0] = np.inf                                                          # non-finite -> 0 on the codec's scale
+    return r.astype(np.float32), g, b
+
+
+def _dwa_want(shape, names, raw_img, types):
+    """The decoded R, G, B of DWA_DECODED's chunks (HALF channels: half bit
+    patterns; FLOAT: the samples), raw chunks as stored, as float32."""
+    H, W = shape
+    out = {}
+    for n in names:
+        half = types.get(n, True)
+        a = np.zeros((H, W), np.uint16 if half else np.float32)
+        for (y0, x0), d in DWA_DECODED[n].items():
+            a[y0:y0 + d.shape[0], x0:x0 + d.shape[1]] = d
+        out[n] = a.view(np.float16).astype(np.float32) if half else a
+    for _, y0, ln, x0, w in RAW_CHUNKS:  # chunks DWA would not shrink are stored as they are
+        for n in names:
+            v = raw_img[n][y0:y0 + ln, x0:x0 + w]
+            out[n][y0:y0 + ln, x0:x0 + w] = v.astype(np.float16).astype(np.float32) if types.get(n, True) else v
+    return out
+
+
+@pytest.mark.parametrize("comp", [8, 9])
+@pytest.mark.parametrize("shape,tile", [((41, 29), None), ((300, 21), None), ((3, 9), None), ((67, 53), (32, 16))])
+@pytest.mark.parametrize("version,ac_mode", [(2, 0), (2, 1), (1, 0)])
+def test_exr_dwa(tmp_path, comp, shape, tile, version, ac_mode):
+    """DWAA / DWAB (OpenImageIO reads them, bmfr.cpp:145-163): an R, G, B set
+    of HALF channels through the lossy DCT with the colour transform, an
+    alpha (RLE) and a FLOAT depth channel (UNKNOWN) in the same chunks,
+    static-Huffman and deflated AC terms, version-2 rules and version 1's
+    fixed set, partial 8x8 blocks and partial chunks (DWAB: 256 lines), tiles.
+    Bit for bit against the decode exr_dwa_py.py predicts from the
+    coefficients it wrote; and close to the input (the codec is lossy)."""
+    H, W = shape
+    r, g, b = _dwa_image(H, W, H * W + comp)
+    chans = {"R": r, "G": g, "B": b, "A": np.full((H, W), 0.5, np.float32), "Z": (r * 100).astype(np.float32)}
+    types = {"Z": False}
+    path = str(tmp_path / "dwa.exr")
+    DWA_DECODED.clear()
+    RAW_CHUNKS.clear()
+    DWA_OPTS.update(version=version, ac_mode=ac_mode, drop=0.02)
+    try:
+        write_exr_py(path, chans, comp, True, tile=tile, types=types)
+    finally:
+        DWA_OPTS.update(version=2, ac_mode=0, drop=0.02)
+    out = np.empty((H, W, 3), np.float32)
+    assert lib().bmfr_exr_read_rgb(path.encode(), W, H, out.ctypes.data) == 0, lib().bmfr_io_error()
+    want = _dwa_want((H, W), "RGB", chans, types)
+    for c, n in enumerate("RGB"):
+        np.testing.assert_array_equal(out[..., c], want[n], err_msg=n)
+    # lossy, but close: relative error on the finite samples
+    for c, src in enumerate((r, g, b)):
+        fin = np.isfinite(src)
+        err = np.abs(out[..., c][fin] - src[fin]) / np.maximum(np.abs(src[fin]), 0.05)
+        assert np.median(err) < 0.05, (c, np.median(err))
+    assert len(RAW_CHUNKS) < len(DWA_DECODED["R"]) or H * W < 64  # DWA-coded chunks (tiny images: stored)
+
+
+def test_exr_dwa_partial_colour_set(tmp_path):
+    """R and G without a HALF B (here FLOAT: an UNKNOWN channel) form no
+    colour set: each is its own lossy decoder, no colour transform."""
+    H, W = 20, 19
+    r, g, b = _dwa_image(H, W, 5)
+    chans = {"R": r, "G": g, "B": b}
+    types = {"B": False}
+    path = str(tmp_path / "dwa_rg.exr")
+    DWA_DECODED.clear()
+    RAW_CHUNKS.clear()
+    write_exr_py(path, chans, 8, True, types=types)
+    out = np.empty((H, W, 3), np.float32)
+    assert lib().bmfr_exr_read_rgb(path.encode(), W, H, out.ctypes.data) == 0, lib().bmfr_io_error()
+    want = _dwa_want((H, W), "RGB", chans, types)
+    for c, n in enumerate("RGB"):
+        np.testing.assert_array_equal(out[..., c], want[n], err_msg=n)
+    np.testing.assert_array_equal(out[..., 2], b)  # UNKNOWN: lossless
+
+
+def test_exr_dwa_rejects_corrupt_chunks(tmp_path):
+    """Bad sizes, an unknown version or AC mode, and a truncated AC stream
+    are errors, not crashes (the ASan corpus in test_sanitizers.py covers
+    random damage)."""
+    H, W = 32, 64
+    r, g, b = _dwa_image(H, W, 9)
+    path = tmp_path / "dwa.exr"
+    DWA_DECODED.clear()
+    RAW_CHUNKS.clear()
+    write_exr_py(str(path), {"R": r, "G": g, "B": b}, 8, True)
+    data = path.read_bytes()
+    p = 8
+    while data[p]:  # attributes: name, type, size, value
+        e2 = data.index(b"\0", data.index(b"\0", p) + 1)
+        p = e2 + 5 + struct.unpack_from("<i", data, e2 + 1)[0]
+    first = struct.unpack_from("<Q", data, p + 1)[0] + 8  # the first chunk's DWA sizes (after y, size)
+    assert struct.unpack_from("<Q", data, first)[0] == 2
+    out = np.empty((H, W, 3), np.float32)
+    for field, value in ((0, 7), (10, 5), (8, 10 ** 6), (9, 3)):  # version, AC mode, AC count, DC count
+        bb = bytearray(data)
+        struct.pack_into("<Q", bb, first + 8 * field, value)
+        (tmp_path / "bad.exr").write_bytes(bytes(bb))
+        assert lib().bmfr_exr_read_rgb(str(tmp_path / "bad.exr").encode(), W, H, out.ctypes.data) != 0, field
+        assert b"corrupt chunk" in lib().bmfr_io_error()

@@ -4,8 +4,8 @@ CPU side):
 
 * the CPU restatement oracle/bmfr_oracle.c, all five stages over several
   configurations (tests/native/oracle_asan_main.c);
-* the EXR reader host/image_io.cpp (PIZ, PXR24 and B44 / B44A decoders,
-  scanline and tiled files) -- the one component that parses external files -- over a
+* the EXR reader host/image_io.cpp (PIZ, PXR24, B44 / B44A and DWAA / DWAB
+  decoders, scanline and tiled files) -- the one component that parses external files -- over a
   corpus of malformed files derived from valid ones:
   every truncation length of a small file, seeded random byte corruption,
   and hand-made hostile headers (huge chunk offsets, attribute sizes past
@@ -23,7 +23,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from test_image_io import _attr, _img, write_exr_py
+from test_image_io import DWA_OPTS, _attr, _dwa_image, _img, write_exr_py
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-g", "-O1"]
@@ -91,10 +91,20 @@ def test_exr_reader_malformed_corpus_under_asan_ubsan(tmp_path):
     for comp, half, tile in ((0, False, None), (1, False, None), (2, True, None), (3, False, None),
                              (4, False, None), (4, True, None), (5, False, None), (5, True, None),
                              (6, True, None), (7, True, None), (7, True, (4, 4)),
-                             (3, False, (4, 4)), (4, False, (8, 2)), (5, False, (4, 4))):
+                             (3, False, (4, 4)), (4, False, (8, 2)), (5, False, (4, 4)),
+                             (8, True, None), (9, True, None), (8, True, (16, 16)), (-8, True, None)):
         name = f"{comp}_{int(half)}" + (f"_t{tile[0]}x{tile[1]}" if tile else "")
         src = tmp_path / f"valid_{name}.exr"
-        write_exr_py(str(src), {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2]}, comp, half=half, tile=tile)
+        if abs(comp) >= 8:  # DWA: an image the codec shrinks (tiny noisy ones are stored raw); -8: deflated AC
+            r, g, b = _dwa_image(24, 40, 3)
+            chans = {"R": r, "G": g, "B": b, "A": np.full(r.shape, 0.5, np.float32), "Z": r * 10}
+            DWA_OPTS.update(ac_mode=int(comp < 0))
+            try:
+                write_exr_py(str(src), chans, abs(comp), half=True, tile=tile, types={"Z": False})
+            finally:
+                DWA_OPTS.update(ac_mode=0)
+        else:
+            write_exr_py(str(src), {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2]}, comp, half=half, tile=tile)
         data = src.read_bytes()
         corpus.append(str(src))
         for n in range(0, len(data), max(1, len(data) // 97)):  # truncations
