@@ -55,6 +55,9 @@ struct K1Lds {
     float mm[3 * (B - 3)];               // per scaled feature: min, max, 1/(max-min)
     int flag;                            // one-launch frame: index of this block's completion flag
     int delay;                           // Params::debug_delay (diagnostics)
+    // Phase 1 -> 3: each row's previous accumulated filtered colour, blended
+    // at the noisy accumulation's taps (bmfr.cl:786-842), [(s * 3 + ch) * kThreads + t]
+    float keep[kSubs * 3 * kThreads];
 };
 
 // ---------------------------------------------------------------------------
@@ -336,7 +339,12 @@ __device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K
         cur[s] = noisy_load_current<IN>(P, in, bx * kEdge + (t & (kEdge - 1)), by * kEdge + (t >> 5) + 8 * s, frame);
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {
-        const NoisyItem it = noisy_item_spec<false, IN>(P, in, A.cam, cur[s], frame);
+        // with accumulate_filtered_data's taps (FILT): the same taps and
+        // weights, so phase 3 needs no second gather
+        const NoisyItem it = noisy_item_spec<true, IN>(P, in, A.cam, cur[s], frame, A.acc_prev);
+        L.keep[(s * 3 + 0) * kThreads + t] = it.prev_f.x;
+        L.keep[(s * 3 + 1) * kThreads + t] = it.prev_f.y;
+        L.keep[(s * 3 + 2) * kThreads + t] = it.prev_f.z;
         over = max(over, it.over);
 #pragma unroll
         for (int f = 0; f < B; ++f) {
@@ -346,7 +354,8 @@ __device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K
             if (__builtin_isnan(v)) v = 0.0f;           // bmfr.cl:468-469
             M.set(f, s, v);
         }
-        const uint32_t bits = (uint32_t)it.owner | ((uint32_t)it.accept << 1) | ((uint32_t)it.spp << 8);
+        const uint32_t bits = (uint32_t)it.owner | ((uint32_t)it.accept << 1) | ((uint32_t)it.prev_f_divided << 5) |
+                              ((uint32_t)it.spp << 8);
         if (s < 2) state |= bits << (16 * s);
         else state_hi |= bits << (16 * (s - 2));
         // owners only (bmfr.cl:478-484), as branch-free stores (st3_drop)
@@ -410,10 +419,8 @@ __device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K
     int t3 = t;  // opaque copy: recompute phase-1 addresses instead of keeping them live
     asm volatile("" : "+v"(t3));
     const int2 off = kBlockOffsets[frame & 15];
-    // All loads of the four rows first (normal, position, reprojection), then
-    // the colours and the previous accumulation's taps.
+    // The normal and position loads of the four rows first.
     f3 n[kSubs], pos[kSubs];
-    float2 pp[kSubs];
     uint32_t lin[kSubs];
     uint32_t bits[kSubs];
 #pragma unroll
@@ -425,7 +432,6 @@ __device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K
         lin[s] = pix(P, (bits[s] & 1u) ? px : P.ox, (bits[s] & 1u) ? py : P.oy);
         n[s] = ld3in<IN>(in.n_cur, lin[s]);
         pos[s] = ld3in<IN>(in.p_cur, lin[s]);
-        pp[s] = ld_px(A.prev_pixel_out, lin[s]);
     }
 #pragma unroll
     for (int s = 0; s < kSubs; ++s) {
@@ -447,8 +453,13 @@ __device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K
             c.x = c.x < 0.f ? 0.f : c.x;
             c.y = c.y < 0.f ? 0.f : c.y;
             c.z = c.z < 0.f ? 0.f : c.z;
-            const f3 acc = blend_filtered(P, c, pp[s].x, pp[s].y, (uint8_t)((bits[s] >> 1) & 15u),
-                                          (uint8_t)(bits[s] >> 8), A.acc_prev, frame);
+            // bmfr.cl:834-849 (blend_filtered's arithmetic, the sums from phase 1):
+            // alpha from the current spp when the taps carried weight
+            const float alpha = (bits[s] & 32u) ? fmaxf(1.f / (float)(bits[s] >> 8), P.second_blend_alpha) : 1.f;
+            const float beta = 1.f - alpha;
+            const f3 prev{L.keep[(s * 3) * kThreads + t3], L.keep[(s * 3 + 1) * kThreads + t3],
+                          L.keep[(s * 3 + 2) * kThreads + t3]};
+            const f3 acc{alpha * c.x + beta * prev.x, alpha * c.y + beta * prev.y, alpha * c.z + beta * prev.z};
             if constexpr (COH) st3_coh(coh_plane(A.acc_out), lin[s], acc);
             else st3(A.acc_out, lin[s], acc);
         }
@@ -468,8 +479,14 @@ __device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K
     }
 }
 
+// Minimum waves per SIMD for the register allocator at B = 13: four (128
+// VGPRs, 12-32 bytes of spills) instead of three (129-130 VGPRs).
+#ifndef BMFR_ROWS_MIN_WAVES
+#define BMFR_ROWS_MIN_WAVES 4
+#endif
+constexpr int kRowsMinWaves = BMFR_ROWS_MIN_WAVES;
 template <int NS, int FS, class IN, bool FAST = false>
-__global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
+__global__ __launch_bounds__(kThreads, FS == 6 ? kRowsMinWaves : 3) void k_fused(Params P, K1Args A) {
     __shared__ K1Lds<NS + FS + 3> L;
     k1_rows_body<NS, FS, IN, false, FAST>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
 }
@@ -478,7 +495,7 @@ __global__ __launch_bounds__(kThreads) void k_fused(Params P, K1Args A) {
 // frame's TAA tiles waiting on their completion flags (as k_fused_cols_taa,
 // bmfr_fused_cols.hip).
 template <int NS, int FS, class IN, bool FAST = false>
-__global__ __launch_bounds__(kThreads) void k_fused_rows_taa(Params P, K1Args A, TaaArgs T, int nk1, int nk1p) {
+__global__ __launch_bounds__(kThreads, FS == 6 ? kRowsMinWaves : 3) void k_fused_rows_taa(Params P, K1Args A, TaaArgs T, int nk1, int nk1p) {
     __shared__ union {
         K1Lds<NS + FS + 3> k1;
         FrameTaaLds<kThreads> k2;

@@ -68,9 +68,11 @@ def time_one(W, H, frames=45, first=5):
     import torch
 
     import bmfr_amd
-    # AB_FAST_FIT=1: time the fast_fit configuration
+    # AB_FAST_FIT=1: time the fast_fit configuration; AB_F32TMP=1: f32 tmp_data
     den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H,
-                                                fast_fit=int(os.environ.get("AB_FAST_FIT", "0"))))
+                                                fast_fit=int(os.environ.get("AB_FAST_FIT", "0")),
+                                                use_half_precision_in_tmp_data=0 if os.environ.get("AB_F32TMP") == "1"
+                                                else 1))
     fr = [bmfr_amd.synth_frame_device(W, H, f) for f in range(frames)]
     den.set_profiling(True, capacity=frames, stride=1)
     for f in range(frames):
