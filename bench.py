@@ -44,13 +44,15 @@ border times and halo bytes come back in `ranks`.  --scaling weak instead
 gives every rank a --width x --height tile.  Timing: barrier + synchronize
 around K frames (exchange included), max over ranks.
 
-Untiled per-frame runs (the N = 1 `value`): a frame is one launch (K1
-blocks, then the frame's TAA tiles, include/bmfr.h); HIP events around
-every timed frame on its stream give that kernel's duration
-(`device_ms_per_frame`, `roofline.launch_ms`), and `kernel_ms` -- K1 and K2
-timed as separate launches -- comes from an untimed second pass over the
-same frames with libbmfr's per-kernel events.  Sequence and tiled runs
-record libbmfr's per-kernel events on every 10th timed frame.
+Untiled per-frame runs (the N = 1 `value`): below 4096 K1 blocks (1080p) a
+frame is one launch (K1 blocks, then the frame's TAA tiles, include/bmfr.h
+bmfr_sizes.frame_launches); HIP events around every timed frame on its
+stream give that kernel's duration (`device_ms_per_frame`,
+`roofline.launch_ms`), and `kernel_ms` -- K1 and K2 timed as separate
+launches -- comes from an untimed second pass over the same frames with
+libbmfr's per-kernel events.  Larger frames (4K, 8K) are two launches, K1
+then K2; they, sequence and tiled runs record libbmfr's per-kernel events
+(on the launch stream) on every 10th timed frame.
 
 Extra JSON fields: `roofline` for the dominant kernel of the timed region
 (the one-launch frame kernel, with the frame's algorithmic bytes; K1 where
@@ -311,7 +313,7 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     # untimed pass with libbmfr's per-kernel events (which time the two as
     # separate launches).  Elsewhere the per-kernel events run inside the
     # timed region on every PROF_STRIDE-th frame.
-    one_launch = grid is None and per_frame
+    one_launch = grid is None and per_frame and cfg.sizes().frame_launches == 1
     stride = PROF_STRIDE if steps >= PROF_STRIDE else 1
     fev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if one_launch else None
 
@@ -442,10 +444,18 @@ def side_line(r):
             "psnr_db": round(r["psnr"], 2)}
 
 
-def variant_line(r, s: int, W: int, H: int, workload: str, kernel: str):
+def variant_line(r, s: int, W: int, H: int, workload: str, kernel: str, k1_kernel: str):
     """A same-size configuration field of the N = 1 line (BASELINE config 5,
-    f32 tmp_data): side_line plus the roofline of its one-launch frame kernel
-    (the frame's 18 s + 74 B/px over the kernel's HIP-event duration)."""
+    f32 tmp_data): side_line plus the roofline of its dominant kernel -- the
+    one-launch frame kernel (the frame's 18 s + 74 B/px over the kernel's
+    HIP-event duration), or K1 where the frame is two launches."""
+    if r["frame_kernel_ms"] is None:
+        kb = k1_bytes_per_px(s) * W * H
+        ka = kb / (r["k1_ms"] * 1e-3) / 1e9
+        return dict(side_line(r), workload=workload,
+                    roofline={"bound": "hbm", "achieved": round(ka, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(ka / HBM_PEAK_GBS, 4), "kernel": k1_kernel + " (K1; frame = K1, K2)",
+                              "algorithmic_bytes_per_launch": kb, "launch_ms": round(r["k1_ms"], 4)})
     fb = frame_bytes_per_px(s) * W * H
     fa = fb / (r["frame_kernel_ms"] * 1e-3) / 1e9
     return dict(side_line(r), workload=workload,
@@ -584,10 +594,12 @@ def main():
                    "algorithmic_bytes_per_launch": k1_bytes_per_px(s) * tile_px}
         if world == 1:
             k1_roof.update(valu_roofline(a.fast_fit))
-        # Untiled per-frame runs with half tmp_data: the frame is one launch
-        # (K1 blocks + TAA tiles), the dominant -- only -- kernel of the timed
-        # region; its roofline is the frame's algorithmic bytes over its
-        # duration, and K1's own (timed apart, untimed pass) is roofline_k1.
+        # Untiled per-frame runs below kTwoLaunchBlocks K1 blocks (bmfr_sizes
+        # frame_launches): the frame is one launch (K1 blocks + TAA tiles),
+        # the dominant -- only -- kernel of the timed region; its roofline is
+        # the frame's algorithmic bytes over its duration, and K1's own (timed
+        # apart, untimed pass) is roofline_k1.  Larger frames are two launches
+        # and K1, timed live by libbmfr's events, is the dominant kernel.
         one_launch = r["frame_kernel_ms"] is not None
         if one_launch:
             fb = frame_bytes_per_px(s) * tile_px
@@ -671,7 +683,8 @@ def main():
             wl = f"bmfr_{W}x{H}_B{rv['cfg'].buffer_count}_{'half' if b.half_tmp else 'f32'}tmp" + \
                  ("_f16in" if b.input_half else "") + ("_fastfit" if b.fast_fit else "")
             line[f"ms_per_frame_{key}"] = variant_line(rv, vs, W, H, wl, "k_fused_cols_taa<..., SAME = true>"
-                                                       if b.half_tmp else "k_fused_rows_taa<...>")
+                                                       if b.half_tmp else "k_fused_rows_taa<...>",
+                                                       "k_fused_cols" if b.half_tmp else "k_fused")
         if world == 1 and a.cpu_frames > 0:
             line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_frames, a.seed)
         print(json.dumps(line), flush=True)

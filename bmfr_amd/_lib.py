@@ -68,6 +68,7 @@ class Sizes(C.Structure):
         ("mins_maxs_bytes", C.c_size_t), ("image_bytes", C.c_size_t),
         ("region_x", C.c_int), ("region_y", C.c_int), ("region_width", C.c_int), ("region_height", C.c_int),
         ("region_bytes", C.c_size_t),
+        ("frame_launches", C.c_int),
     ]
 
 

@@ -303,6 +303,7 @@ bmfr_status bmfr_config_sizes(const bmfr_config* c, bmfr_sizes* s) {
         s->region_height = c->image_height;
     }
     s->region_bytes = (size_t)s->region_width * s->region_height * 3 * sizeof(float);
+    s->frame_launches = s->blocks >= bmfr::kTwoLaunchBlocks ? 2 : 1;  // launch_fused_frame's rule
     return BMFR_OK;
 }
 

@@ -287,9 +287,15 @@ hipError_t launch_fused_k2(const Params& P, hipStream_t st, const FusedArgs& A) 
 hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& A, hipEvent_t mid) {
     hipError_t e;
     // One launch for the frame, unless K1 and K2 are timed apart (mid event).
-#ifndef BMFR_FRAME_TWO_LAUNCH
-    if (!mid && A.done && frame_fused_supported(P)) return launch_fused_frame_one(P, st, A);
-#endif
+    // One launch for the frame (K1 blocks, then the TAA tiles waiting on their
+    // completion flags) below kTwoLaunchBlocks K1 blocks; above, K1 and K2
+    // as two launches, where K2 runs at its own occupancy (90 VGPRs, five
+    // waves per SIMD; inside the frame kernel it has K1's four) and the gap
+    // between the launches is small beside the frame: measured (round 4,
+    // profiles/r04_bench_two_launch.txt) 4K 0.3758 -> 0.3711, 8K 1.409 ->
+    // 1.365, f32 tmp_data 0.444 -> 0.425 ms/frame, but 1080p 0.111 -> 0.118.
+    if (!mid && A.done && frame_fused_supported(P) && k1_blocks(P) < kTwoLaunchBlocks)
+        return launch_fused_frame_one(P, st, A);
     if (fused_supported(P)) {
         if ((e = launch_fused_k1_blocks(P, st, A)) != hipSuccess) return e;
         if (mid) (void)hipEventRecord(mid, st);

@@ -74,6 +74,12 @@ inline TaaArgs taa_args(const FusedArgs& A) {
 bool fitter_supported(int not_scaled, int scaled);
 // Work-groups of a K1 launch (the rectangle, or its ring).
 inline int k1_blocks(const Params& P) { return P.ring > 0 ? P.ring : P.nbx * P.nby; }
+// launch_fused_frame: frames of at least this many K1 blocks run as two
+// launches (K1, K2) instead of one (-DBMFR_FRAME_TWO_LAUNCH_BLOCKS=N).
+#ifndef BMFR_FRAME_TWO_LAUNCH_BLOCKS
+#define BMFR_FRAME_TWO_LAUNCH_BLOCKS 4096
+#endif
+constexpr int kTwoLaunchBlocks = BMFR_FRAME_TWO_LAUNCH_BLOCKS;
 bool fused_supported(const Params& P);
 // The canonical path tone-maps in K2 (bmfr.cl:851-856), for each tile pixel
 // and its 1-px halo.  f32 tmp_data: row-split K1 (bmfr_fused.hip).

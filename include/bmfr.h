@@ -149,6 +149,12 @@ typedef struct bmfr_sizes {
      * [region_x, region_x + region_width) x [region_y, region_y + region_height). */
     int region_x, region_y, region_width, region_height;
     size_t region_bytes;    /* one float3 plane of the region */
+    /* Kernel launches of an untiled bmfr_process_frame on the fused path
+     * (canonical feature lists; profiling off): 1 (K1 blocks, then the TAA
+     * tiles on completion flags) for frames below 4096 K1 blocks (`blocks`),
+     * 2 (K1, then K2) from there -- measured faster at 4K / 8K, slower at
+     * 1080p. */
+    int frame_launches;
 } bmfr_sizes;
 
 typedef struct bmfr_ctx bmfr_ctx;

@@ -53,6 +53,8 @@ def test_config_sizes_match_reference(W, H, third, half):
     want = reference_sizes(W, H, 4, 9 if third else 6, half)
     got = {k: getattr(s, k) for k in want}
     assert got == want
+    # untiled per-frame launches: one below 4096 K1 blocks, two from there
+    assert s.frame_launches == (2 if s.blocks >= 4096 else 1)
 
 
 @pytest.mark.parametrize("W,H", [(40, 64), (64, 40), (46, 100), (33, 33), (0, 10), (31, 200)])

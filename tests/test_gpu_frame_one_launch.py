@@ -3,8 +3,12 @@ the TAA tiles of a frame wait on completion flags of the K1 blocks under
 them and read their outputs device-coherent) against the same frames run as
 two launches (K1, then K2: what a profiled frame does), bit for bit on the
 output and every temporal-state plane, at the BASELINE sizes and a small
-odd size.  The full-size reference tests (test_gpu_reference_fullsize.py)
-pin the one-launch path to the reference kernels as well."""
+odd size.  Frames of 4096 K1 blocks or more (4K) run as two launches
+unprofiled too (bmfr_sizes.frame_launches): there the per-frame path is
+checked against the profiled one; the one-launch kernel at full size runs
+in the tiled contexts' border launches (test_gpu_tiled.py).  The full-size
+reference tests (test_gpu_reference_fullsize.py) pin both paths to the
+reference kernels as well."""
 import pytest
 import torch
 
@@ -37,6 +41,8 @@ def run(W, H, frames, profiled):
 
 @pytest.mark.parametrize("W,H,frames", [(3840, 2160, 5), (1920, 1080, 8), (200, 136, 20)])
 def test_one_launch_frame_equals_two_launches(W, H, frames, gpu):
+    launches = bmfr_amd.BmfrConfig(image_width=W, image_height=H).sizes().frame_launches
+    assert launches == (2 if W >= 3840 else 1)
     one, two = run(W, H, frames, False), run(W, H, frames, True)
     for f in range(frames):
         for k in one[f]:

@@ -4,8 +4,9 @@ include/bmfr_debug.h bmfr_debug_sync).
 
 Two waits exist: a K1 wave waiting in LDS for the Householder pivot another
 wave of its work-group publishes (bmfr_fused_cols.hip wait_flag), and, in
-the one-launch frame, a TAA tile waiting for the completion flags of the K1
-blocks under it (bmfr_taa_tile.h wait_k1_blocks)."""
+the one-launch frame (frames below 4096 K1 blocks, bmfr_sizes.frame_launches;
+4K and up run K1 and K2 as two launches), a TAA tile waiting for the
+completion flags of the K1 blocks under it (bmfr_taa_tile.h wait_k1_blocks)."""
 from __future__ import annotations
 
 import pytest
@@ -47,20 +48,21 @@ def test_default_bounds_report_ok(gpu):
     assert den.frame_status() == 0
 
 
-@pytest.mark.parametrize("half_tmp", [1, 0])
-def test_exhausted_waits_report_sync_timeout(half_tmp, gpu):
+@pytest.mark.parametrize("W,H,half_tmp", [(3840, 2160, 1), (2560, 1440, 1), (2560, 1440, 0)])
+def test_exhausted_waits_report_sync_timeout(W, H, half_tmp, gpu):
     """max_polls = 0: a wait gives up at the first flag that is not ready yet.
-    At 4K thousands of K1 blocks wait for pivots and the TAA tiles in K1's
-    tail wait for blocks still running, so the frame must report; the report
-    is sticky (the next frame's call returns it) until frame 0."""
-    W, H = 3840, 2160
+    Thousands of K1 blocks wait for pivots (half tmp_data) and, in the
+    one-launch frame (2560x1440: 3726 K1 blocks), the TAA tiles in K1's tail
+    wait for blocks still running, so the frame must report; the report is
+    sticky (the next frame's call returns it) until frame 0."""
+    assert bmfr_amd.BmfrConfig(image_width=W, image_height=H).sizes().frame_launches == (2 if W == 3840 else 1)
     den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H,
                                                 use_half_precision_in_tmp_data=half_tmp))
     frames = _frames(W, H, 3)
     den.debug_sync(max_polls=0)
     _run(den, frames[:2])
-    # half tmp_data: K1's pivot waits and the tiles' waits; f32 (row-split K1,
-    # work-group barriers): the tiles' waits of the one-launch frame
+    # half tmp_data: K1's pivot waits (and the tiles' waits of a one-launch
+    # frame); f32 (row-split K1, work-group barriers): the tiles' waits
     assert den.frame_status() == _lib.SYNC_TIMEOUT
     with pytest.raises(bmfr_amd.BmfrError) as e:
         _run(den, frames[2:3], first=2)
@@ -82,7 +84,7 @@ def test_sequence_api_reports_sync_timeout(gpu):
     assert den.frame_status() == 0
 
 
-@pytest.mark.parametrize("W,H,half_tmp", [(3840, 2160, 1), (1920, 1080, 1), (3840, 2160, 0)])
+@pytest.mark.parametrize("W,H,half_tmp", [(2560, 1440, 1), (1920, 1080, 1), (2560, 1440, 0)])
 def test_delayed_k1_blocks_one_launch_exact(W, H, half_tmp, gpu):
     """One K1 block in 61 sleeps ~0.3 ms before it raises its completion
     flag, so the TAA tiles over it really wait on the flags: the one-launch
