@@ -132,6 +132,7 @@ SIGNATURES = {
     "bmfr_synth_camera": (None, [_I, _I, _I, _F16, _F2]),
     "bmfr_debug_stamps": (_I, [_P, _P, C.c_size_t]),  # include/bmfr_debug.h
     "bmfr_debug_sync": (_I, [_P, _I, _I]),  # include/bmfr_debug.h
+    "bmfr_debug_frame_launches": (_I, [_P, _I]),
     "bmfr_synth_frame_host": (_I, [_I, _I, _I, C.c_uint32, _P, _P, _P, _P, _P]),
     "bmfr_synth_frame_device": (_I, [_I, _I, _I, C.c_uint32, _P, _P, _P, _P, _P, _P]),
     "bmfr_synth_region_device": (_I, [_I, _I, _I, _I, _I, _I, _I, C.c_uint32, _P, _P, _P, _P, _P, _P]),

@@ -181,6 +181,7 @@ Params make_params(const bmfr_config* c, const bmfr_sizes* s) {
     P.wx0 = P.vx0, P.wy0 = P.vy0, P.wx1 = P.vx1, P.wy1 = P.vy1;
     P.max_polls = bmfr::kDefaultMaxPolls;
     P.debug_delay = 0;
+    P.frame_launches = 0;
     return P;
 }
 
@@ -1022,6 +1023,12 @@ bmfr_status bmfr_debug_sync(bmfr_ctx* c, int max_polls, int k1_delay) {
     if (!c || k1_delay < 0 || c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
     c->P.max_polls = max_polls < 0 ? bmfr::kDefaultMaxPolls : max_polls;
     c->P.debug_delay = k1_delay;
+    return BMFR_OK;
+}
+
+bmfr_status bmfr_debug_frame_launches(bmfr_ctx* c, int launches) {
+    if (!c || launches < 0 || launches > 2 || c->pending_frame >= 0) return BMFR_ERROR_INVALID_ARGUMENT;
+    c->P.frame_launches = launches;
     return BMFR_OK;
 }
 

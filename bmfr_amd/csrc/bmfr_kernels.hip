@@ -294,8 +294,8 @@ hipError_t launch_fused_frame(const Params& P, hipStream_t st, const FusedArgs& 
     // between the launches is small beside the frame: measured (round 4,
     // profiles/r04_bench_two_launch.txt) 4K 0.3758 -> 0.3711, 8K 1.409 ->
     // 1.365, f32 tmp_data 0.444 -> 0.425 ms/frame, but 1080p 0.111 -> 0.118.
-    if (!mid && A.done && frame_fused_supported(P) && k1_blocks(P) < kTwoLaunchBlocks)
-        return launch_fused_frame_one(P, st, A);
+    const bool one = P.frame_launches == 1 || (P.frame_launches == 0 && k1_blocks(P) < kTwoLaunchBlocks);
+    if (!mid && A.done && frame_fused_supported(P) && one) return launch_fused_frame_one(P, st, A);
     if (fused_supported(P)) {
         if ((e = launch_fused_k1_blocks(P, st, A)) != hipSuccess) return e;
         if (mid) (void)hipEventRecord(mid, st);

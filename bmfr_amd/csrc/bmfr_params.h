@@ -72,6 +72,10 @@ struct Params {
     // shader cycles before it publishes its completion flag, so TAA tiles
     // really wait.  0: off.
     int debug_delay;
+    // Host side only (launch_fused_frame): kernel launches of an untiled
+    // frame -- 0 by the frame's size (kTwoLaunchBlocks), 1 or 2 forced
+    // (include/bmfr_debug.h bmfr_debug_frame_launches).
+    int frame_launches;
 };
 constexpr int kDefaultMaxPolls = 1 << 20;
 constexpr int kDelayStride = 61, kDelayPhase = 7;

@@ -278,6 +278,11 @@ class Denoiser(_Context):
         a K1 completion delay, for the frames enqueued from now on."""
         check(self.lib.bmfr_debug_sync(self.handle, max_polls, k1_delay), "bmfr_debug_sync")
 
+    def debug_frame_launches(self, launches: int = 0) -> None:
+        """include/bmfr_debug.h bmfr_debug_frame_launches: 0 by frame size (default),
+        1 one launch, 2 K1 then K2, for the untiled frames enqueued from now on."""
+        check(self.lib.bmfr_debug_frame_launches(self.handle, launches), "bmfr_debug_frame_launches")
+
     def set_profiling(self, enable: bool, capacity: int = 4096, stride: int = 1) -> None:
         """stride: record only frames whose number is a multiple of it."""
         check(self.lib.bmfr_set_profiling_stride(self.handle, stride), "bmfr_set_profiling_stride")

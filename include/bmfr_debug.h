@@ -22,6 +22,12 @@ bmfr_status bmfr_debug_stamps(const bmfr_ctx *ctx, unsigned long long *host, siz
  * K1 block in 61 sleeps k1_delay x ~8K shader cycles before it publishes its
  * completion flag, so the TAA tiles really wait (results must not change). */
 bmfr_status bmfr_debug_sync(bmfr_ctx *ctx, int max_polls, int k1_delay);
+/* bmfr_debug_frame_launches: kernel launches of the untiled bmfr_process_frame
+ * from now on -- 0: by the frame's size (bmfr_sizes.frame_launches, the
+ * default), 1: one launch (K1 blocks, then the TAA tiles on completion
+ * flags) at any size, 2: K1, then K2.  Results are the same bit for bit;
+ * the tests use it to run the one-launch kernel at 4K. */
+bmfr_status bmfr_debug_frame_launches(bmfr_ctx *ctx, int launches);
 #ifdef __cplusplus
 }
 #endif

@@ -5,10 +5,10 @@ two launches (K1, then K2: what a profiled frame does), bit for bit on the
 output and every temporal-state plane, at the BASELINE sizes and a small
 odd size.  Frames of 4096 K1 blocks or more (4K) run as two launches
 unprofiled too (bmfr_sizes.frame_launches): there the per-frame path is
-checked against the profiled one; the one-launch kernel at full size runs
-in the tiled contexts' border launches (test_gpu_tiled.py).  The full-size
-reference tests (test_gpu_reference_fullsize.py) pin both paths to the
-reference kernels as well."""
+checked against the profiled one, and the one-launch kernel is forced
+(include/bmfr_debug.h bmfr_debug_frame_launches) and checked as well.  The
+full-size reference tests (test_gpu_reference_fullsize.py) pin the default
+paths to the reference kernels."""
 import pytest
 import torch
 
@@ -17,8 +17,9 @@ import bmfr_amd
 pytestmark = pytest.mark.gpu
 
 
-def run(W, H, frames, profiled):
+def run(W, H, frames, profiled, launches=0):
     den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    den.debug_frame_launches(launches)
     if profiled:  # per-kernel events on every frame: K1 and K2 as two launches
         den.set_profiling(True, capacity=frames, stride=1)
     n = W * H
@@ -43,10 +44,14 @@ def run(W, H, frames, profiled):
 def test_one_launch_frame_equals_two_launches(W, H, frames, gpu):
     launches = bmfr_amd.BmfrConfig(image_width=W, image_height=H).sizes().frame_launches
     assert launches == (2 if W >= 3840 else 1)
-    one, two = run(W, H, frames, False), run(W, H, frames, True)
-    for f in range(frames):
-        for k in one[f]:
-            a, b = one[f][k], two[f][k]
-            if a.dtype == torch.float32:
-                a, b = a.view(torch.int32), b.view(torch.int32)
-            assert torch.equal(a, b), f"frame {f} {k}: {int((a != b).sum())} of {a.numel()} differ"
+    two = run(W, H, frames, True)
+    runs = {"default": run(W, H, frames, False)}
+    if launches == 2:  # the one-launch kernel at this size too
+        runs["one launch"] = run(W, H, frames, False, launches=1)
+    for name, one in runs.items():
+        for f in range(frames):
+            for k in one[f]:
+                a, b = one[f][k], two[f][k]
+                if a.dtype == torch.float32:
+                    a, b = a.view(torch.int32), b.view(torch.int32)
+                assert torch.equal(a, b), f"{name}: frame {f} {k}: {int((a != b).sum())} of {a.numel()} differ"
