@@ -699,9 +699,6 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // (76-144 bytes) hold too many registers for it.
     constexpr bool kKeepNP = FAST && B < 16;
     In3<IN> keep_n[NI], keep_p[NI];
-#ifdef BMFR_K1_P1_PRIO
-    __builtin_amdgcn_s_setprio(BMFR_K1_P1_PRIO);  // experiment: phase 1 (the gathers) ahead of other work-groups' fits
-#endif
     NoisyCur<IN> cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly, frame);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -755,9 +752,6 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     float pre[kPre][kSlots];
     WaveFit<NS, FS, NW, FAST>::prefetch_noise(w, l, A.noise, pre);
     k1_barrier();  // matrix in LDS; phase 1's global stores drain in the background
-#ifdef BMFR_K1_P1_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
     BMFR_STAMP(1);
     BMFR_STAMP(2);  // scaling runs inside the per-wave fit
 
