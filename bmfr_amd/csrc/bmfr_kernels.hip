@@ -110,7 +110,13 @@ __global__ __launch_bounds__(256) void k_taa(Params P, const float2* __restrict_
 // bmfr_taa_tile.h).
 // Tile height measured at 4K (K2 ms): 8: 0.114, 12: 0.105, 16: 0.112,
 // 24: 0.130, 32: 0.135; forcing 4 waves/SIMD (128 VGPRs) at 16: 0.159.
-constexpr int kTaaW = 64, kTaaH = 12;
+// Round 4 (taps after the tone map, -DBMFR_K2_H / -DBMFR_K2_NT): 12: 0.1028,
+// 8 (80 VGPRs, six waves): 0.1028, 16: 0.1062, 512 threads x 16: 0.1074,
+// 512 x 24: 0.1190 (profiles/r04_ab_k2_shapes.txt).
+#ifndef BMFR_K2_H
+#define BMFR_K2_H 12
+#endif
+constexpr int kTaaW = 64, kTaaH = BMFR_K2_H;
 // Threads per tile (experiment: -DBMFR_K2_NT=384 / 768 -- 2 / 1 output
 // pixels per thread instead of 3, fewer registers, more waves per SIMD).
 #ifndef BMFR_K2_NT
