@@ -680,7 +680,18 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // LDS until the end (fewer scalar registers live across the kernel)
     if constexpr (COH)
         if (t == 0) L.flag = (by - P.by0) * P.nbx + (bx - P.bx0);
-    const int lx = l & (kEdge - 1), ly = (l >> 5) + 2 * NI * w;  // item i: row y = ly + 2 i
+    // Item i of wave w: block row pair 2 (NI w + i) (a wave sweeps its own 8
+    // rows), or with kInterleave 2 (NW i + w) (the work-group's waves sweep
+    // the block together, neighbouring row pairs at a time: their previous-
+    // frame taps share cache lines); lanes 0-31 / 32-63 take the pair's rows.
+    // The design-matrix row of a pixel (its index in the block) is the same
+    // either way: only which thread computes it changes.
+    // kInterleave with fast_fit: K1 -1.1 %; on the exact path +1.1 % (its
+    // half-at-a-time matrix stores), so not there (profiles/r04_ab_row_interleave.txt).
+    constexpr bool kInterleave = FAST;
+    auto item_slot = [&](int i) { return kInterleave ? NW * i + w : NI * w + i; };  // row slot j: rows l + 64 j
+    const int lx = l & (kEdge - 1);
+    auto item_row = [&](int lane, int i) { return (lane >> 5) + 2 * item_slot(i); };
 
     // ---- accumulate_noisy_data (bmfr.cl:310-484), rows l + 64 (NI w + i) ----
     h2 pk[B];            // features of an item pair, packed for one 4-byte LDS store per column
@@ -699,12 +710,12 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // (76-144 bytes) hold too many registers for it.
     constexpr bool kKeepNP = FAST && B < 16;
     In3<IN> keep_n[NI], keep_p[NI];
-    NoisyCur<IN> cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly, frame);
+    NoisyCur<IN> cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + item_row(l, 0), frame);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
         const NoisyTaps<IN> tp = noisy_taps_issue<true, IN>(P, A.in, A.cam, cur, frame, A.acc_prev);
         NoisyCur<IN> nxt;
-        if (i < NI - 1) nxt = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + ly + 2 * (i + 1), frame);
+        if (i < NI - 1) nxt = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + item_row(l, i + 1), frame);
         __builtin_amdgcn_sched_barrier(0);
         const NoisyItem it = noisy_taps_finish<true, IN>(P, cur, tp, frame);
         if constexpr (kKeepNP) {
@@ -720,7 +731,12 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 // NaN -> 0 (bmfr.cl:468-469), then the +-65504 clamp (bmfr.cl:471-473)
                 // as one med3 (equal to fmax(fmin(v, 65504), -65504) for every non-NaN v)
                 v = __builtin_isnan(v) ? 0.0f : __builtin_amdgcn_fmed3f(v, -65504.f, 65504.f);
-                pk[f][i & 1] = (_Float16)v;
+                if constexpr (kInterleave) {  // this item's half of its row-slot pair (XOR-swizzled as below)
+                    const int j = item_slot(i);
+                    L.M[f - 1][l * kSlots + 2 * ((j >> 1) ^ ((l >> 2) & 7)) + (j & 1)] = (_Float16)v;
+                } else {
+                    pk[f][i & 1] = (_Float16)v;
+                }
             }
             spps |= (uint32_t)it.spp << (8 * i);
             ibits |= ((uint32_t)it.owner << i) | ((uint32_t)it.prev_f_divided << (4 + i));
@@ -738,7 +754,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
             st3_drop(drop_plane(A.noisy_out), it.lin, it.owner, it.color);
             st1_drop(drop_plane(A.spp_out), it.lin, it.owner, it.spp);
             st2_drop<COH ? kSc1 : 0>(drop_plane(A.prev_pixel_out), it.lin, it.owner, make_float2(it.pfx, it.pfy));
-            if (i & 1) {  // rows j = NI w + i - 1, NI w + i: adjacent halves of lane l's row slot
+            if (!kInterleave && (i & 1)) {  // rows j = NI w + i - 1, NI w + i: adjacent halves of lane l's row slot
                 // (pair (NI w + i) / 2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)
                 const int pair = ((NI * w + i) / 2) ^ ((l >> 2) & 7);
 #pragma unroll
@@ -768,7 +784,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
         const int px = bx * kEdge + (l3 & (kEdge - 1)) - kEdge / 2 + off.x;
-        const int py = by * kEdge + (l3 >> 5) + 2 * NI * w + 2 * i - kEdge / 2 + off.y;
+        const int py = by * kEdge + item_row(l3, i) - kEdge / 2 + off.y;
         lin[i] = pix(P, (ibits & (1u << i)) ? px : P.ox, (ibits & (1u << i)) ? py : P.oy);  // margins: a valid pixel, skipped below
         if constexpr (kKeepNP) {
             nrm_r[i] = keep_n[i];
