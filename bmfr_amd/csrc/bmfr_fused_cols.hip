@@ -688,8 +688,16 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // either way: only which thread computes it changes.
     // kInterleave with fast_fit: K1 -1.1 %; on the exact path +1.1 % (its
     // half-at-a-time matrix stores), so not there (profiles/r04_ab_row_interleave.txt).
-    constexpr bool kInterleave = FAST;
-    auto item_slot = [&](int i) { return kInterleave ? NW * i + w : NI * w + i; };  // row slot j: rows l + 64 j
+#ifndef BMFR_K1_INTERLEAVE
+#define BMFR_K1_INTERLEAVE (FAST ? 1 : 0)
+#endif
+    // 0: own 8 rows; 1: slot NW i + w; 2: item pairs interleaved (slots 2 NW (i / 2) + 2 w + (i & 1):
+    // a thread's two items of a pair stay adjacent slots, one 4-byte store per column)
+    constexpr int kIlv = BMFR_K1_INTERLEAVE;
+    constexpr bool kInterleave = kIlv == 1;
+    auto item_slot = [&](int i) {  // row slot j: rows l + 64 j
+        return kIlv == 1 ? NW * i + w : (kIlv == 2 ? 2 * NW * (i / 2) + 2 * w + (i & 1) : NI * w + i);
+    };
     const int lx = l & (kEdge - 1);
     auto item_row = [&](int lane, int i) { return (lane >> 5) + 2 * item_slot(i); };
 
@@ -756,7 +764,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
             st2_drop<COH ? kSc1 : 0>(drop_plane(A.prev_pixel_out), it.lin, it.owner, make_float2(it.pfx, it.pfy));
             if (!kInterleave && (i & 1)) {  // rows j = NI w + i - 1, NI w + i: adjacent halves of lane l's row slot
                 // (pair (NI w + i) / 2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)
-                const int pair = ((NI * w + i) / 2) ^ ((l >> 2) & 7);
+                const int pair = (item_slot(i) / 2) ^ ((l >> 2) & 7);
 #pragma unroll
                 for (int f = 1; f < B; ++f)
                     *reinterpret_cast<uint32_t*>(&L.M[f - 1][l * kSlots + 2 * pair]) = __builtin_bit_cast(uint32_t, pk[f]);
