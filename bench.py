@@ -145,10 +145,12 @@ def parse(argv=None):
     ap.add_argument("--sequence", action="store_true",
                     help="single GPU: the timed frames as one bmfr_process_sequence call (TAA of frame f beside "
                          "K1 of frame f+1) instead of one bmfr_process_frame per frame")
-    ap.add_argument("--exchange", choices=("native", "torch"), default="native",
-                    help="multi-GPU over RCCL: native = libbmfr's bmfr_exchange_run (pack + grouped ncclSend / "
-                         "ncclRecv + unpack, one C call per frame); torch = torch.distributed isend / irecv between "
-                         "libbmfr's pack / unpack (gloo rehearsals always use torch)")
+    ap.add_argument("--exchange", choices=("native", "torch"), default="torch",
+                    help="multi-GPU over RCCL: torch (default) = torch.distributed isend / irecv between libbmfr's "
+                         "pack / unpack kernels -- the path the gloo rehearsals run end to end; native = libbmfr's "
+                         "bmfr_exchange_run (pack + grouped ncclSend / ncclRecv + unpack, one C call per frame), "
+                         "whose RCCL branch has not yet run between two ranks (tests/test_gpu_exchange.py "
+                         "test_rccl_two_gpus_matches_untiled needs a multi-GPU box)")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="multi-GPU: exchange the halo before the frame instead of under K1's interior blocks")
     a = ap.parse_args(argv)
@@ -250,9 +252,10 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     scratch = spin_up(a, cfg, local, frames, cams)  # its last frames still run under the warm-up frames
     transport = None
     if grid:
-        # RCCL: libbmfr's native exchange (one C call per frame enqueues pack, the grouped
-        # ncclSend / ncclRecv batch and unpack); gloo (the one-GPU rehearsal) or
-        # --exchange torch: torch.distributed point-to-point between libbmfr's pack / unpack
+        # torch.distributed point-to-point (RCCL with the nccl backend; gloo, host-staged, in the
+        # one-GPU rehearsal) between libbmfr's pack / unpack kernels; --exchange native: libbmfr's
+        # own exchange (one C call per frame enqueues pack, the grouped ncclSend / ncclRecv batch
+        # and unpack)
         transport = tiling.DistTransport(grid, rank, dev, host_staging=backend != "nccl")
         if backend == "nccl" and a.exchange == "native":
             comm_handle = tiling.RcclComm(world, rank, local)

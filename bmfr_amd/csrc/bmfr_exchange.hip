@@ -295,6 +295,10 @@ bmfr_status bmfr_exchange_create(bmfr_ctx* ctx, const bmfr_config* cfg, const in
     (void)bmfr_state(ctx, 0, &v);
     hipPointerAttribute_t attr;
     x->device = hipPointerGetAttributes(&attr, v.result) == hipSuccess ? attr.device : (prev >= 0 ? prev : 0);
+    if (comm && comm->device != x->device) {  // RCCL would move sbuf / rbuf of another GPU
+        delete x;
+        return BMFR_ERROR_INVALID_ARGUMENT;
+    }
     (void)hipSetDevice(x->device);
     hipError_t e = hipSuccess;
     if (x->scap) e = hipMalloc(&x->sbuf, x->scap);
@@ -393,24 +397,42 @@ bmfr_status bmfr_exchange_run_all(bmfr_exchange* const* xs, int n, void* const* 
         for (int i = 0; i < n && st == BMFR_OK; ++i) st = unpack(xs[i], reinterpret_cast<hipStream_t>(streams[i]), f);
         return st;
     }
-    // no communicator: every context on one device, one stream (streams[0]);
-    // rank i's messages packed into its send buffer and unpacked straight into
-    // the receivers (the receiver's records for i are the sender's for it)
+    // No communicator: every context on one device, one stream (streams[0]).
+    // The RCCL path's buffers exactly, with each ncclSend / ncclRecv pair
+    // replaced by one device copy: every rank packs its send_all records into
+    // its sbuf; each message then moves from the sender's sbuf (at the
+    // sender's offset for that peer) into the receiver's rbuf (at the
+    // receiver's offset for the sender); every rank unpacks its recv_all
+    // records from its rbuf.  A message whose two ends disagree on its size is
+    // a plan error (the RCCL receive would be truncated or wait forever).
     for (int i = 1; i < n; ++i)
         if (xs[i]->device != xs[0]->device) return BMFR_ERROR_UNSUPPORTED;
     const hipStream_t s = reinterpret_cast<hipStream_t>(streams[0]);
-    for (int i = 0; i < n && st == BMFR_OK; ++i) {
+    for (int i = 0; i < n && st == BMFR_OK; ++i) st = pack(xs[i], s, f);
+    if (st != BMFR_OK) return st;
+    for (int i = 0; i < n; ++i) {  // receiver i
         bmfr_exchange* x = xs[i];
-        if ((st = pack(x, s, f)) != BMFR_OK) return st;
-        size_t so = 0;
+        size_t ro = 0;
         for (const auto& p : x->plans[f]) {
-            if (p.send_bytes)
-                st = bmfr_halo_copy(xs[p.peer]->ctx, s, p.send.data(), (int)p.send.size() / 5, x->sbuf + so, 1,
-                                    nullptr);
-            if (st != BMFR_OK) return st;
-            so += p.send_bytes;
+            if (p.recv_bytes) {
+                const bmfr_exchange* y = xs[p.peer];  // the sender
+                size_t so = 0;
+                const PeerPlan* q = nullptr;
+                for (const auto& yp : y->plans[f]) {
+                    if (yp.peer == i) {
+                        q = &yp;
+                        break;
+                    }
+                    so += yp.send_bytes;
+                }
+                if (!q || q->send_bytes != p.recv_bytes || q->send != p.recv) return BMFR_ERROR_INVALID_ARGUMENT;
+                const hipError_t e = hipMemcpyAsync(x->rbuf + ro, y->sbuf + so, p.recv_bytes, hipMemcpyDeviceToDevice, s);
+                if (e != hipSuccess) return hip_st(e);
+            }
+            ro += p.recv_bytes;
         }
     }
+    for (int i = 0; i < n && st == BMFR_OK; ++i) st = unpack(xs[i], s, f);
     return st;
 }
 

@@ -759,8 +759,19 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 L.keep_s[(i * 3 + 2) * NT + t] = it.prev_f.z;
             }
             // owners only (bmfr.cl:478-484), as branch-free stores (st3_drop)
+#if defined(BMFR_PROBE_K1_REC16)
+            {
+                typedef unsigned u4 __attribute__((ext_vector_type(4)));
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    u4{__float_as_uint(it.color.x), __float_as_uint(it.color.y), __float_as_uint(it.color.z), it.spp},
+                    drop_plane(A.noisy_out), it.owner ? it.lin * 16u : kDropOff, 0, 0);
+            }
+#else
             st3_drop(drop_plane(A.noisy_out), it.lin, it.owner, it.color);
+#endif
+#if !defined(BMFR_PROBE_K1_REC) && !defined(BMFR_PROBE_K1_REC16)
             st1_drop(drop_plane(A.spp_out), it.lin, it.owner, it.spp);
+#endif
             st2_drop<COH ? kSc1 : 0>(drop_plane(A.prev_pixel_out), it.lin, it.owner, make_float2(it.pfx, it.pfy));
             if (!kInterleave && (i & 1)) {  // rows j = NI w + i - 1, NI w + i: adjacent halves of lane l's row slot
                 // (pair (NI w + i) / 2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)

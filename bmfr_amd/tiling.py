@@ -222,6 +222,20 @@ def _rect_array(rects):
     return (C.c_int * max(5 * len(recs), 1))(*[v for r in recs for v in r])
 
 
+def packed_bytes(records) -> int:
+    """bmfr_halo_copy's packed size of bmfr_halo_copy records (x, y, w, h,
+    planes), host only: rectangle after rectangle, plane after plane, each
+    segment padded to 16 bytes (include/bmfr.h) -- the message size both ends
+    of an exchange compute (bmfr_amd/csrc/bmfr_capi.hip bmfr_halo_copy)."""
+    bpp = [b for _, b in STATE_PLANES]
+    total = 0
+    for x, y, w, h, mask in records:
+        for k, b in enumerate(bpp):
+            if mask & (1 << k):
+                total += (w * b * h + 15) & ~15
+    return total
+
+
 def halo_bytes(denoiser, rects) -> int:
     """Packed size of the rectangles' segments (bmfr_halo_copy layout)."""
     from ._lib import check

@@ -340,6 +340,7 @@ int run_tiled(const Options& o, const bmfr_config& base, const Camera& cam, cons
         bmfr_sizes sz;
         int device = 0;
         hipStream_t stream = nullptr;
+        hipEvent_t joined = nullptr;  // one-GPU runs: the stream join around the exchange
         float* in[2][4] = {};  // current / previous region planes: noisy, normal, position, albedo
         bmfr_exchange* x = nullptr;
     };
@@ -361,6 +362,7 @@ int run_tiled(const Options& o, const bmfr_config& base, const Camera& cam, cons
         BMFR_CHECK(bmfr_get_sizes(q.ctx, &q.sz));
         HIP_CHECK(hipSetDevice(q.device));
         HIP_CHECK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&q.joined, hipEventDisableTiming));  // reused every frame
         for (auto& s : q.in)
             for (auto& p : s) HIP_CHECK(hipMalloc(&p, q.sz.region_bytes));
         BMFR_CHECK(bmfr_exchange_create(q.ctx, &q.cfg, tiles.data(), T, r, comms[r], &q.x));
@@ -397,22 +399,15 @@ int run_tiled(const Options& o, const bmfr_config& base, const Camera& cam, cons
             for (int r = 0; r < T; ++r)
                 BMFR_CHECK(bmfr_process_frame_interior(t[r].ctx, t[r].stream, &in[r],
                                                        &cam.matrices[16 * matrix_index], &cam.offsets[2 * f], f));
-            if (o.gpus == 1) {  // one stream carries the device copies: join every tile's stream onto it
+            if (o.gpus == 1)  // one stream carries the device copies: join every tile's stream onto it
                 for (int r = 1; r < T; ++r) {
-                    hipEvent_t e;
-                    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-                    HIP_CHECK(hipEventRecord(e, t[r].stream));
-                    HIP_CHECK(hipStreamWaitEvent(t[0].stream, e, 0));
-                    HIP_CHECK(hipEventDestroy(e));
+                    HIP_CHECK(hipEventRecord(t[r].joined, t[r].stream));
+                    HIP_CHECK(hipStreamWaitEvent(t[0].stream, t[r].joined, 0));
                 }
-            }
             BMFR_CHECK(bmfr_exchange_run_all(xs.data(), T, streams.data(), f));
             if (o.gpus == 1) {
-                hipEvent_t e;
-                HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-                HIP_CHECK(hipEventRecord(e, t[0].stream));
-                for (int r = 1; r < T; ++r) HIP_CHECK(hipStreamWaitEvent(t[r].stream, e, 0));
-                HIP_CHECK(hipEventDestroy(e));
+                HIP_CHECK(hipEventRecord(t[0].joined, t[0].stream));
+                for (int r = 1; r < T; ++r) HIP_CHECK(hipStreamWaitEvent(t[r].stream, t[0].joined, 0));
             }
             for (int r = 0; r < T; ++r)
                 BMFR_CHECK(bmfr_process_frame_border(t[r].ctx, t[r].stream, &in[r],
@@ -462,6 +457,7 @@ int run_tiled(const Options& o, const bmfr_config& base, const Camera& cam, cons
         for (auto& s : q.in)
             for (auto& p : s) (void)hipFree(p);
         (void)hipStreamDestroy(q.stream);
+        (void)hipEventDestroy(q.joined);
         bmfr_destroy(q.ctx);
         if (comms[r]) bmfr_comm_destroy(comms[r]);
     }

@@ -735,6 +735,14 @@ bool uncompress(const ExrHeader& h, const uint8_t* in, size_t n, int width, int 
 //     LOSSY_DCT channels, in channel-list order.
 // Parity is unpinned: no OpenEXR library and no reference DWA file exist
 // here; tests/exr_dwa_py.py is an independent encoder of the same scheme.
+// Why the last chunk decode failed when the file is valid but uses a feature
+// this reader does not implement ("" = corrupt data); the caller reports it.
+thread_local std::string g_chunk_unsupported;
+bool unsupported(const std::string& what) {
+    g_chunk_unsupported = what;
+    return false;
+}
+
 namespace dwa {
 
 enum Scheme { kUnknown = 0, kLossyDct = 1, kRle = 2 };
@@ -916,8 +924,16 @@ bool uncompress(const ExrHeader& h, const uint8_t* in, size_t n, int width, int 
             }
         }
     }
-    for (size_t i = 0; i < nc; ++i)
-        if (scheme[i] == kLossyDct && h.channels[i].type != kHalf) return false;
+    // LOSSY_DCT channels hold halves; a FLOAT channel under a LOSSY_DCT rule
+    // (OpenEXR's version-2 default rules list R, G, B, Y, BY, RY for HALF and
+    // FLOAT) is decoded as half and widened to float.  UINT cannot be lossy.
+    // A pLinear channel would skip the perceptual-to-linear table in some
+    // writers: without a reference decoder to pin that here it is refused.
+    for (size_t i = 0; i < nc; ++i) {
+        if (scheme[i] != kLossyDct) continue;
+        if (h.channels[i].type == kUint) return false;
+        if (h.channels[i].linear) return unsupported("DWA pLinear channel " + h.channels[i].name);
+    }
 
     // per-channel decoded planes (row-major, type_bytes per sample)
     std::vector<std::vector<uint8_t>> plane(nc);
@@ -996,7 +1012,7 @@ bool uncompress(const ExrHeader& h, const uint8_t* in, size_t n, int width, int 
     size_t ai = 0, di = 0;
     for (const auto& dec : decoders) {
         const size_t k = dec.size();
-        for (int c : dec) plane[c].assign(W * L * 2, 0);
+        for (int c : dec) plane[c].assign(W * L * type_bytes(h.channels[c].type), 0);
         for (size_t b = 0; b < nb; ++b) {
             float blk[3][64];
             for (size_t c = 0; c < k; ++c) {
@@ -1031,9 +1047,14 @@ bool uncompress(const ExrHeader& h, const uint8_t* in, size_t n, int width, int 
                 for (size_t dy = 0; dy < 8 && y0 + dy < L; ++dy)
                     for (size_t dx = 0; dx < 8 && x0 + dx < W; ++dx) {
                         const uint16_t v = lin[float_to_half(blk[c][dy * 8 + dx])];
-                        uint8_t* o = plane[dec[c]].data() + ((y0 + dy) * W + x0 + dx) * 2;
-                        o[0] = (uint8_t)(v & 0xff);
-                        o[1] = (uint8_t)(v >> 8);
+                        if (h.channels[dec[c]].type == kFloat) {  // widened exactly
+                            const float f = half_to_float(v);
+                            std::memcpy(plane[dec[c]].data() + ((y0 + dy) * W + x0 + dx) * 4, &f, 4);
+                        } else {
+                            uint8_t* o = plane[dec[c]].data() + ((y0 + dy) * W + x0 + dx) * 2;
+                            o[0] = (uint8_t)(v & 0xff);
+                            o[1] = (uint8_t)(v >> 8);
+                        }
                     }
         }
         di += k * nb;
@@ -1194,6 +1215,7 @@ int bmfr_exr_read_rgb(const char* path, int width, int height, float* rgb) {
     size_t px_bytes = 0;  // all channels of one pixel
     for (const Channel& c : h.channels) px_bytes += type_bytes(c.type);
     std::vector<uint8_t> raw;
+    g_chunk_unsupported.clear();
     if (h.tiled) {
         // Level (0, 0): the first nx * ny entries of the offset table (tiles
         // in row-major order; the other levels of a mip / rip map follow).
@@ -1213,7 +1235,8 @@ int bmfr_exr_read_rgb(const char* path, int width, int height, float* rgb) {
             const int x0 = (int)(hd[0] * (int64_t)h.tile_w), y0 = (int)(hd[1] * (int64_t)h.tile_h);
             const int w = std::min((int)h.tile_w, width - x0), lines = std::min((int)h.tile_h, height - y0);
             if (!decode_chunk(h, file.data() + off + 20, (size_t)hd[4], px_bytes * w * lines, w, lines, raw))
-                return fail(std::string(path) + ": corrupt tile " + std::to_string(hd[0]) + "," + std::to_string(hd[1]));
+                return fail(std::string(path) + (g_chunk_unsupported.empty() ? ": corrupt tile " : ": unsupported: " +
+                            g_chunk_unsupported + ", tile ") + std::to_string(hd[0]) + "," + std::to_string(hd[1]));
             scatter(raw, x0, w, y0, lines);
         }
         return 0;
@@ -1234,7 +1257,8 @@ int bmfr_exr_read_rgb(const char* path, int width, int height, float* rgb) {
             return fail(std::string(path) + ": bad chunk");
         const int lines = std::min(lpc, height - line0);
         if (!decode_chunk(h, file.data() + off + 8, (size_t)size, px_bytes * width * lines, width, lines, raw))
-            return fail(std::string(path) + ": corrupt chunk at y=" + std::to_string(y));
+            return fail(std::string(path) + (g_chunk_unsupported.empty() ? ": corrupt chunk" : ": unsupported: " +
+                        g_chunk_unsupported + ",") + " at y=" + std::to_string(y));
         scatter(raw, 0, width, line0, lines);
     }
     return 0;

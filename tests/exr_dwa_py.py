@@ -47,6 +47,10 @@ DEFAULT_RULES = [("R", 0, LOSSY_DCT, True, HALF), ("G", 1, LOSSY_DCT, True, HALF
                  ("Y", -1, LOSSY_DCT, True, HALF), ("BY", -1, LOSSY_DCT, True, HALF),
                  ("RY", -1, LOSSY_DCT, True, HALF), ("A", -1, RLE, True, UINT), ("A", -1, RLE, True, HALF),
                  ("A", -1, RLE, True, FLOAT)]
+# OpenEXR's version-2 default rules also list the colour / luminance names for
+# FLOAT channels (stored as halves, widened on decode).
+DEFAULT_RULES_FLOAT = DEFAULT_RULES + [(n, c, LOSSY_DCT, True, FLOAT) for n, c in
+                                       (("R", 0), ("G", 1), ("B", 2), ("Y", -1), ("BY", -1), ("RY", -1))]
 LEGACY_RULES = [("r", 0, LOSSY_DCT, True, HALF), ("red", 0, LOSSY_DCT, True, HALF), ("g", 1, LOSSY_DCT, True, HALF),
                 ("grn", 1, LOSSY_DCT, True, HALF), ("green", 1, LOSSY_DCT, True, HALF),
                 ("b", 2, LOSSY_DCT, True, HALF), ("blu", 2, LOSSY_DCT, True, HALF),
@@ -252,7 +256,9 @@ def dwa_compress(chans: dict, types: dict, lines: int, w: int, version: int = 2,
         for n, o in zip(dec, out):
             with np.errstate(over="ignore"):
                 hb = o.astype(np.float16).view(np.uint16)
-            decoded[n] = _unblock(TO_LINEAR[hb], lines, w)
+            d = _unblock(TO_LINEAR[hb], lines, w)
+            # a FLOAT lossy channel: the half, widened exactly
+            decoded[n] = d.view(np.float16).astype(np.float32) if types[n] == FLOAT else d
     # sections
     unk_c = zlib.compress(bytes(unk)) if unk else b""
     if ac_words:

@@ -13,7 +13,7 @@ import pytest
 import torch
 
 import bmfr_amd
-from bmfr_amd.tiling import HipCopier, NativeExchange, TileGrid, halo_rects, state_planes
+from bmfr_amd.tiling import HipCopier, NativeExchange, TileGrid, halo_bytes, halo_rects, packed_bytes, state_planes
 
 pytestmark = pytest.mark.gpu
 
@@ -65,6 +65,85 @@ def test_native_exchange_matches_untiled(shape, fast_fit, gpu):
             sent = sum(x.bytes(f)[0] for x in xs)
             recv = sum(x.bytes(f)[1] for x in xs)
             assert sent == recv > 0
+            for r, x in enumerate(xs):  # the host mirror of the packed layout (tests/test_tiling.py)
+                plan = grid.frame_plan(r, f)
+                assert x.bytes(f) == (sum(packed_bytes(s) for _, s, _ in plan),
+                                      sum(packed_bytes(q) for _, _, q in plan))
+                for _, s, q in plan:
+                    for recs in (s, q):
+                        if recs:
+                            assert halo_bytes(tiles[r], recs) == packed_bytes(recs)
+
+
+def _multi_gpu_run(W, H, tx, ty, halo, frames, fast_fit):
+    """Each tile of a tx x ty grid on its own GPU (devices 0..n-1 of this
+    process), the halo exchange through RCCL communicators made by
+    bmfr_comm_create_all (every rank's ncclSend / ncclRecv in one group),
+    compared with the untiled frame on device 0."""
+    import ctypes as C
+
+    from bmfr_amd import _lib
+    lib = _lib.load()
+    grid = TileGrid(W, H, tx, ty, halo=halo)
+    n = grid.ranks
+    devs = (C.c_int * n)(*range(n))
+    comms = (C.c_void_p * n)()
+    assert lib.bmfr_comm_create_all(n, devs, comms) == 0
+    full = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H, fast_fit=fast_fit), device=0)
+    tiles = [bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H, tile=grid.tile(r), tile_halo=halo,
+                                                   fast_fit=fast_fit), device=r) for r in range(n)]
+
+    class _C:
+        def __init__(self, h):
+            self.handle = h
+
+    xs = [NativeExchange(d, grid, r, _C(comms[r])) for r, d in enumerate(tiles)]
+    streams = [torch.cuda.Stream(device=r) for r in range(n)]
+    prev = [None] * n
+    for f in range(frames):
+        vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))
+        _, jit = bmfr_amd.synth_camera(W, H, f)
+        fr = bmfr_amd.synth_frame_device(W, H, f)
+        full.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], vp, jit, f)
+        inps = []
+        for r, d in enumerate(tiles):
+            with torch.cuda.device(r):
+                inps.append(bmfr_amd.synth_region_device(W, H, d.region, f, device=r, stream=streams[r]))
+        if f > 0:
+            NativeExchange.run_all(xs, f, streams)
+        for r, d in enumerate(tiles):
+            kw = dict(prev_normals=prev[r]["normals"], prev_positions=prev[r]["positions"]) if prev[r] else {}
+            i = inps[r]
+            with torch.cuda.device(r):
+                d.process_frame(i["noisy"], i["normals"], i["positions"], i["albedo"], vp, jit, f, stream=streams[r],
+                                **kw)
+        prev = inps
+        for r in range(n):
+            torch.cuda.synchronize(r)
+        want = full.copy_output(torch.empty(3 * W * H, device="cuda:0")).view(H, W, 3)
+        for r, d in enumerate(tiles):
+            assert d.halo_status() == 0
+            rx, ry, rw, rh = d.region
+            x, y, w, h = grid.tile(r)
+            with torch.cuda.device(r):
+                got = d.copy_output(torch.empty(3 * rw * rh, device=f"cuda:{r}"), stream=streams[r]).view(rh, rw, 3)
+                torch.cuda.synchronize(r)
+            a = got[y - ry:y - ry + h, x - rx:x - rx + w].contiguous().cpu().view(torch.int32)
+            b = want[y:y + h, x:x + w].contiguous().cpu().view(torch.int32)
+            assert torch.equal(a, b), (f, r, int((a != b).sum()))
+    for x in xs:
+        x.close()
+    for r in range(n):
+        assert lib.bmfr_comm_destroy(comms[r]) == 0
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL between ranks needs two GPUs")
+@pytest.mark.parametrize("fast_fit", [0, 1])
+def test_rccl_two_gpus_matches_untiled(fast_fit, gpu):
+    """The RCCL branch of bmfr_exchange_run_all (pack, one grouped ncclSend /
+    ncclRecv batch over the grid's communicators, unpack) on a 2 x 1 grid of
+    two GPUs == the untiled frame bit for bit (skipped on one-GPU boxes)."""
+    _multi_gpu_run(320, 256, 2, 1, 40, 6, fast_fit)
 
 
 def test_rccl_single_rank_communicators(gpu):

@@ -645,6 +645,51 @@ def test_exr_dwa_partial_colour_set(tmp_path):
     np.testing.assert_array_equal(out[..., 2], b)  # UNKNOWN: lossless
 
 
+def test_exr_dwa_float_lossy_channels(tmp_path):
+    """FLOAT R, G, B under OpenEXR's version-2 default rules, which mark them
+    LOSSY_DCT too: decoded as halves (colour transform included) and widened
+    exactly to float."""
+    H, W = 24, 37
+    r, g, b = _dwa_image(H, W, 11)
+    chans = {"R": r, "G": g, "B": b}
+    types = {"R": False, "G": False, "B": False}
+    path = str(tmp_path / "dwa_f.exr")
+    DWA_DECODED.clear()
+    RAW_CHUNKS.clear()
+    DWA_OPTS.update(rules=exr_dwa_py.DEFAULT_RULES_FLOAT)
+    try:
+        write_exr_py(path, chans, 9, True, types=types)
+    finally:
+        DWA_OPTS.pop("rules")
+    assert not RAW_CHUNKS
+    out = np.empty((H, W, 3), np.float32)
+    assert lib().bmfr_exr_read_rgb(path.encode(), W, H, out.ctypes.data) == 0, lib().bmfr_io_error()
+    want = _dwa_want((H, W), "RGB", chans, types)
+    for c, n in enumerate("RGB"):
+        np.testing.assert_array_equal(out[..., c], want[n], err_msg=n)
+        assert (want[n] == want[n].astype(np.float16).astype(np.float32)).all()  # halves, widened
+
+
+def test_exr_dwa_rejects_plinear_lossy_channel(tmp_path):
+    """A LOSSY_DCT channel with the pLinear flag is refused as unsupported
+    (not reported as corrupt data)."""
+    H, W = 32, 64
+    r, g, b = _dwa_image(H, W, 13)
+    path = tmp_path / "dwa_lin.exr"
+    DWA_DECODED.clear()
+    RAW_CHUNKS.clear()
+    write_exr_py(str(path), {"R": r, "G": g, "B": b}, 8, True)
+    assert not RAW_CHUNKS
+    bb = bytearray(path.read_bytes())
+    i = bb.index(b"G\0", bb.index(b"chlist"))
+    bb[i + 2 + 4] = 1  # G's pLinear flag
+    path.write_bytes(bytes(bb))
+    out = np.empty((H, W, 3), np.float32)
+    assert lib().bmfr_exr_read_rgb(str(path).encode(), W, H, out.ctypes.data) != 0
+    err = lib().bmfr_io_error()
+    assert b"unsupported" in err and b"pLinear" in err and b"corrupt" not in err, err
+
+
 def test_exr_dwa_rejects_corrupt_chunks(tmp_path):
     """Bad sizes, an unknown version or AC mode, and a truncated AC stream
     are errors, not crashes (the ASan corpus in test_sanitizers.py covers

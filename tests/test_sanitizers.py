@@ -23,6 +23,7 @@ import subprocess
 import numpy as np
 import pytest
 
+import exr_dwa_py
 from test_image_io import DWA_OPTS, _attr, _dwa_image, _img, write_exr_py
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -92,17 +93,23 @@ def test_exr_reader_malformed_corpus_under_asan_ubsan(tmp_path):
                              (4, False, None), (4, True, None), (5, False, None), (5, True, None),
                              (6, True, None), (7, True, None), (7, True, (4, 4)),
                              (3, False, (4, 4)), (4, False, (8, 2)), (5, False, (4, 4)),
-                             (8, True, None), (9, True, None), (8, True, (16, 16)), (-8, True, None)):
+                             (8, True, None), (9, True, None), (8, True, (16, 16)), (-8, True, None),
+                             (9, False, None)):
         name = f"{comp}_{int(half)}" + (f"_t{tile[0]}x{tile[1]}" if tile else "")
         src = tmp_path / f"valid_{name}.exr"
-        if abs(comp) >= 8:  # DWA: an image the codec shrinks (tiny noisy ones are stored raw); -8: deflated AC
+        if abs(comp) >= 8:  # DWA: an image the codec shrinks (tiny noisy ones are stored raw); -8: deflated AC;
+            # (9, False): FLOAT R, G, B under the FLOAT LOSSY_DCT rules (decoded as halves, widened)
             r, g, b = _dwa_image(24, 40, 3)
             chans = {"R": r, "G": g, "B": b, "A": np.full(r.shape, 0.5, np.float32), "Z": r * 10}
+            types = {"Z": False} if half else {"R": False, "G": False, "B": False, "Z": False}
             DWA_OPTS.update(ac_mode=int(comp < 0))
+            if not half:
+                DWA_OPTS.update(rules=exr_dwa_py.DEFAULT_RULES_FLOAT)
             try:
-                write_exr_py(str(src), chans, abs(comp), half=True, tile=tile, types={"Z": False})
+                write_exr_py(str(src), chans, abs(comp), half=True, tile=tile, types=types)
             finally:
                 DWA_OPTS.update(ac_mode=0)
+                DWA_OPTS.pop("rules", None)
         else:
             write_exr_py(str(src), {"R": img[..., 0], "G": img[..., 1], "B": img[..., 2]}, comp, half=half, tile=tile)
         data = src.read_bytes()
@@ -119,6 +126,13 @@ def test_exr_reader_malformed_corpus_under_asan_ubsan(tmp_path):
             p.write_bytes(bytes(b))
             corpus.append(str(p))
     hostile = _hostile(tmp_path)
+    # a DWA file whose lossy G channel carries the pLinear flag: refused
+    src = tmp_path / "valid_8_1.exr"
+    b = bytearray(src.read_bytes())
+    i = b.index(b"G\0", b.index(b"chlist"))
+    b[i + 2 + 4] = 1
+    (tmp_path / "dwa_plinear.exr").write_bytes(bytes(b))
+    hostile.append(str(tmp_path / "dwa_plinear.exr"))
     out = _run([exe, *corpus, *hostile])
     assert f"files {len(corpus) + len(hostile)}" in out, out
     # every hostile file is rejected, every valid one read

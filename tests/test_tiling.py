@@ -205,6 +205,43 @@ def test_native_plan_equals_frame_plan(W, H, tx, ty, halo):
             assert tiling.native_plan(cfg, g, r, f) == want, (r, f)
 
 
+@pytest.mark.parametrize("W,H,tx,ty,halo", [(320, 256, 2, 2, 40), (480, 288, 4, 2, 38), (352, 224, 1, 2, 48),
+                                            (7680, 4320, 4, 2, 64), (7680, 4320, 2, 4, 64)])
+def test_native_messages_match_at_both_ends(W, H, tx, ty, halo):
+    """Every message of libbmfr's exchange plan (bmfr_halo_plan, what
+    bmfr_exchange_* posts as one ncclSend / ncclRecv pair) is described the
+    same way at both ends, for every rank and all 16 block-grid shifts: the
+    sender's records for a peer equal that peer's receive records from it,
+    hence the packed byte counts agree (packed_bytes == bmfr_halo_copy's
+    layout; a mismatch would truncate an RCCL receive or leave it waiting).
+    The messages are also laid out in the send / receive buffers in peer
+    order at both ends, which the device-copy form of bmfr_exchange_run_all
+    reproduces (tests/test_gpu_exchange.py)."""
+    import bmfr_amd
+    from bmfr_amd import tiling
+    cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H)
+    g = tiling.TileGrid(W, H, tx, ty, halo=halo)
+    for f in range(16):
+        plans = {r: {p: (s, q) for p, s, q in tiling.native_plan(cfg, g, r, f)} for r in range(g.ranks)}
+        total_sent = total_recv = 0
+        for r, peers in plans.items():
+            for p, (send, recv) in peers.items():
+                assert r in plans[p], (f, r, p)
+                assert plans[p][r][1] == send, (f, r, p)  # the peer receives what I send
+                assert plans[p][r][0] == recv, (f, r, p)  # and sends what I receive
+                assert tiling.packed_bytes(send) == tiling.packed_bytes(plans[p][r][1])
+                total_sent += tiling.packed_bytes(send)
+                total_recv += tiling.packed_bytes(recv)
+        assert total_sent == total_recv > 0
+
+
+def test_packed_bytes_pads_segments():
+    from bmfr_amd.tiling import HALO_ALL, HALO_RESULT, packed_bytes
+    # 3 x 1 px: noisy 36 -> 48, spp 3 -> 16, filtered 36 -> 48, result 36 -> 48
+    assert packed_bytes([(0, 0, 3, 1, HALO_ALL)]) == 48 + 16 + 48 + 48
+    assert packed_bytes([(0, 0, 4, 4, HALO_RESULT), (5, 5, 1, 1, 2)]) == 192 + 16
+
+
 def test_native_plan_rejects_bad_grids():
     import ctypes as C
 
