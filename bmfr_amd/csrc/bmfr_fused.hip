@@ -455,7 +455,8 @@ __device__ __forceinline__ void k1_rows_body(const Params& P, const K1Args& A, K
             c.z = c.z < 0.f ? 0.f : c.z;
             // bmfr.cl:834-849 (blend_filtered's arithmetic, the sums from phase 1):
             // alpha from the current spp when the taps carried weight
-            const float alpha = (bits[s] & 32u) ? fmaxf(1.f / (float)(bits[s] >> 8), P.second_blend_alpha) : 1.f;
+            // 1 / spp, spp in [1, 255] (rcp_nr: exactly 1.f / spp)
+            const float alpha = (bits[s] & 32u) ? fmaxf(rcp_nr((float)(bits[s] >> 8)), P.second_blend_alpha) : 1.f;
             const float beta = 1.f - alpha;
             const f3 prev{L.keep[(s * 3) * kThreads + t3], L.keep[(s * 3 + 1) * kThreads + t3],
                           L.keep[(s * 3 + 2) * kThreads + t3]};

@@ -893,9 +893,12 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
             ci.y = ci.y < 0.f ? 0.f : ci.y;
             ci.z = ci.z < 0.f ? 0.f : ci.z;
             // bmfr.cl:834-849: alpha from the current spp when the taps carried weight
-            const float alpha = (ibits & (1u << (4 + i)))
-                                    ? fmaxf(1.f / (float)((spps >> (8 * i)) & 255u), P.second_blend_alpha)
-                                    : 1.f;
+            // 1 / spp with spp in [1, 255]: rcp_nr (exactly 1.f / spp); the
+            // one-launch frame kernel keeps the division (rcp_nr's shorter
+            // sequence is scheduled early there and spills 14-17 VGPRs)
+            const float sp = (float)((spps >> (8 * i)) & 255u);
+            const float alpha =
+                (ibits & (1u << (4 + i))) ? fmaxf(COH ? 1.f / sp : rcp_nr(sp), P.second_blend_alpha) : 1.f;
             const float beta = 1.f - alpha;
             const int t3 = l3 + 64 * w;
             const float* kb = L.keep();

@@ -85,11 +85,11 @@ struct NoisyItem {
     uint8_t spp;
     bool owner;       // pixel_without_mirror inside the image
     // noisy_item_spec<true> only: the previous accumulated filtered colour
-    // at the same taps, blended as accumulate_filtered_data does
-    // (bmfr.cl:786-842) -- prev_f (divided by the tap weight sum when > 0)
-    // and alpha_f, so acc = alpha_f * filtered + (1 - alpha_f) * prev_f.
+    // at the same taps, as accumulate_filtered_data sums it (bmfr.cl:786-842)
+    // -- prev_f, divided by the tap weight sum when that is > 0; the blend
+    // acc = alpha_f * filtered + (1 - alpha_f) * prev_f with alpha_f from the
+    // new spp happens where the filtered colour is known (phase 3).
     f3 prev_f;
-    float alpha_f;
     bool prev_f_divided;  // the tap weights summed to > 0 (alpha_f from spp)
     int over;             // noisy_item_spec, P.check_reach: px by which an in-image tap leaves [vx0, vx1) x [vy0, vy1)
                           // ([wx0, wx1) x [wy0, wy1) for a pixel of the output tile)
@@ -471,10 +471,8 @@ __device__ __forceinline__ NoisyItem taps_blend(const Params& P, const f3& cur, 
     f3 prev{0.f, 0.f, 0.f};
     float sample_spp = 0.f;
     o.prev_f = f3{0.f, 0.f, 0.f};
-    o.alpha_f = 1.f;
     o.prev_f_divided = false;
     o.over = over;
-    float tap_total = 0.f;
     if (frame > 0) {
         float total = 0.f;
 #pragma unroll
@@ -498,21 +496,20 @@ __device__ __forceinline__ NoisyItem taps_blend(const Params& P, const f3& cur, 
             prev.y = div_shared(prev.y, total, rt);
             prev.z = div_shared(prev.z, total, rt);
             sample_spp = div_shared(sample_spp, total, rt);
-            alpha = 1.f / (sample_spp + 1.f);
+            // 1 / (sample_spp + 1): sample_spp is a weighted mean of spp
+            // values in [0, 255], so the divisor lies in [1, 257) (rcp_nr)
+            alpha = rcp_nr(sample_spp + 1.f);
             alpha = fmaxf(alpha, P.blend_alpha);
+            if (FILT) {  // bmfr.cl:834-842: the same sum of accepted tap weights, one reciprocal
+                o.prev_f_divided = true;
+                o.prev_f.x = div_shared(o.prev_f.x, total, rt);
+                o.prev_f.y = div_shared(o.prev_f.y, total, rt);
+                o.prev_f.z = div_shared(o.prev_f.z, total, rt);
+            }
         }
-        tap_total = total;
     }
     uint8_t new_spp = 1;  // bmfr.cl:433-442
     if (alpha < 1.f) new_spp = sample_spp > 254.f ? 255 : (uint8_t)((int)rintf(sample_spp) + 1);
-    if (FILT && tap_total > 0.f) {  // bmfr.cl:834-842 (the same sum of accepted tap weights)
-        const float rt = 1.f / tap_total;
-        o.prev_f_divided = true;
-        o.alpha_f = fmaxf(1.f / (float)new_spp, P.second_blend_alpha);
-        o.prev_f.x = div_shared(o.prev_f.x, tap_total, rt);
-        o.prev_f.y = div_shared(o.prev_f.y, tap_total, rt);
-        o.prev_f.z = div_shared(o.prev_f.z, tap_total, rt);
-    }
     const float beta = 1.f - alpha;
     o.color = f3{alpha * cur.x + beta * prev.x, alpha * cur.y + beta * prev.y, alpha * cur.z + beta * prev.z};
     o.pfx = pfx;
@@ -861,6 +858,12 @@ __device__ __forceinline__ f3 taa_history(const Params& P, float2 pf, const f3 (
 // in nb[] for them); without it every neighbour must be in the image.  A
 // skipped neighbour enters the min / max as +inf / -inf, which leaves them
 // unchanged bit for bit, so both forms are upstream's sequence.
+__device__ __forceinline__ f3 taa_clamp_tail(const Params& P, f3 me, f3 mnb, f3 mxb, f3 mnc, f3 mxc, f3 py);
+// The off-screen test of bmfr.cl:884-890: the pixel keeps its own colour.
+__device__ __forceinline__ bool taa_offscreen(const Params& P, float2 pf, int frame) {
+    const float flx = floorf(pf.x), fly = floorf(pf.y);
+    return frame == 0 || flx < -1.f || fly < -1.f || flx >= (float)P.width || fly >= (float)P.height;
+}
 template <bool CHECK>
 __device__ __forceinline__ f3 taa_clamp(const Params& P, int x, int y, f3 me, float2 pf, const f3 (&nb)[9], f3 py,
                                         int frame) {
@@ -902,6 +905,17 @@ __device__ __forceinline__ f3 taa_clamp(const Params& P, int x, int y, f3 me, fl
     box_cross([](const f3& v) { return v.x; }, mnb.x, mxb.x, mnc.x, mxc.x);
     box_cross([](const f3& v) { return v.y; }, mnb.y, mxb.y, mnc.y, mxc.y);
     box_cross([](const f3& v) { return v.z; }, mnb.z, mxb.z, mnc.z, mxc.z);
+    return taa_clamp_tail(P, me, mnb, mxb, mnc, mxc, py);
+}
+
+// taa_clamp's part after the neighbourhood: the history py clamped to the
+// average of the box and cross bounds (bmfr.cl:922-973), blended with me.
+// The min / max of a set are exact and order-independent on v_min / v_max
+// (minNum: a NaN operand is ignored, -0 < +0), so a caller may form the box
+// and cross bounds in any grouping -- e.g. from per-row partial bounds shared
+// by vertically neighbouring pixels -- as long as each set starts from +inf /
+// -inf as upstream's does (an all-NaN set then yields +inf / -inf).
+__device__ __forceinline__ f3 taa_clamp_tail(const Params& P, f3 me, f3 mnb, f3 mxb, f3 mnc, f3 mxc, f3 py) {
     const f3 lo{(mnb.x + mnc.x) / 2.f, (mnb.y + mnc.y) / 2.f, (mnb.z + mnc.z) / 2.f};
     const f3 hi{(mxb.x + mxc.x) / 2.f, (mxb.y + mxc.y) / 2.f, (mxb.z + mxc.z) / 2.f};
     const f3 cl{fminf(fmaxf(py.x, lo.x), hi.x), fminf(fmaxf(py.y, lo.y), hi.y), fminf(fmaxf(py.z, lo.z), hi.z)};

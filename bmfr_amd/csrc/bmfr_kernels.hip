@@ -123,10 +123,11 @@ constexpr int kTaaW = 64, kTaaH = BMFR_K2_H;
 #define BMFR_K2_NT 256
 #endif
 constexpr int kTaaNT = BMFR_K2_NT;
-// Minimum waves per SIMD for the register allocator (experiment knob; the
-// default leaves it free: 90 VGPRs, five waves).
+// Minimum waves per SIMD for the register allocator: six (80 VGPRs, no
+// spills since the strip resolve; K2 0.0989 -> 0.0980 ms against five,
+// profiles/r05_ab_k2.txt).
 #ifndef BMFR_K2_MINW
-#define BMFR_K2_MINW 1
+#define BMFR_K2_MINW 6
 #endif
 template <class IN>
 __global__ __launch_bounds__(kTaaNT, BMFR_K2_MINW) void k_fused_taa(Params P, TaaArgs T) {
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(kTaaNT, BMFR_K2_MINW) void k_fused_taa(Params P, Ta
     const int gi = xcd_swizzle(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int bxi = gi % gridDim.x, byi = gi / gridDim.x;
     forward_reach(T, blockIdx.x == 0 && blockIdx.y == 0);
-    taa_tile<IN, kTaaH, false, kTaaNT>(P, T, P.tx0 + bxi * kTaaW, P.ty0 + byi * kTaaH, Y, sE, sRP);
+    taa_tile<IN, kTaaH, false, kTaaNT, kStrip>(P, T, P.tx0 + bxi * kTaaW, P.ty0 + byi * kTaaH, Y, sE, sRP);
 }
 
 // ------------------------------------------------------------ halo copy --

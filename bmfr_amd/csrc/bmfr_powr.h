@@ -25,7 +25,12 @@ extern "C" __device__ float __ocml_powr_f32(float, float);
 // tables read from `tE` / `tRP`: kPowrE / kPowrRP in global memory, or a
 // work-group's copy in LDS (bmfr_powr_tables_to_lds), which keeps the two
 // lookups per channel off the vector-memory path.
-__device__ __forceinline__ float gamma_clamped(float p, const double* tE = kPowrE, const double2* tRP = kPowrRP) {
+// The table part alone: the result when *rare is false; when *rare is true
+// (the double lies within 2^10 double ulps of a float rounding midpoint) the
+// caller must take gamma_clamped instead.  Branch-free, so a caller can issue
+// the lookups of several values back to back and fix the rare ones after.
+__device__ __forceinline__ float gamma_table(float p, bool& rare, const double* tE = kPowrE,
+                                             const double2* tRP = kPowrRP) {
     const bool pos = p > 0.f, below = p < 1.f;
     const float x = pos && below ? p : 0.5f;
     const float m = __builtin_amdgcn_frexp_mantf(x);
@@ -38,11 +43,54 @@ __device__ __forceinline__ float gamma_clamped(float p, const double* tE = kPowr
     q = __builtin_fma(q, u, BMFR_POWR_A2);
     q = __builtin_fma(q, u, BMFR_POWR_A1);
     const double r = __builtin_fma(ep, u * q, ep);
-    float v = (float)r;
     const uint32_t low = (uint32_t)__double_as_longlong(r) & 0x1FFFFFFFu;
-    if (__builtin_expect(low - (0x10000000u - 1024u) < 2048u, 0))
-        v = (float)__ocml_pow_f64((double)x, (double)0.454545f);
-    return pos ? (below ? v : 1.f) : 0.f;
+    rare = pos && below && low - (0x10000000u - 1024u) < 2048u;
+    return pos ? (below ? (float)r : 1.f) : 0.f;
+}
+
+// gamma_table of three values with the six table lookups issued together
+// (a scheduling barrier keeps the compiler from spacing them out to save
+// registers: each would then wait for its own LDS round trip).  Bit i of
+// *rare: value i needs gamma_clamped.
+__device__ __forceinline__ void gamma_table3(const float (&p)[3], float (&out)[3], uint32_t& rare,
+                                             const double* tE, const double2* tRP) {
+    float m[3];
+    bool ok[3], pos[3], below[3];
+    double2 rp[3];
+    double te[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        pos[c] = p[c] > 0.f;
+        below[c] = p[c] < 1.f;
+        ok[c] = pos[c] && below[c];
+        const float x = ok[c] ? p[c] : 0.5f;
+        m[c] = __builtin_amdgcn_frexp_mantf(x);
+        const int e = __builtin_amdgcn_frexp_expf(x);
+        const int j = (int)(__float_as_uint(m[c]) >> (23 - BMFR_POWR_J_BITS)) & ((1 << BMFR_POWR_J_BITS) - 1);
+        rp[c] = tRP[j];
+        te[c] = tE[e - BMFR_POWR_E_MIN];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    rare = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const double ep = te[c] * rp[c].y;
+        const double u = __builtin_fma((double)m[c], rp[c].x, -1.0);
+        double q = __builtin_fma(BMFR_POWR_A4, u, BMFR_POWR_A3);
+        q = __builtin_fma(q, u, BMFR_POWR_A2);
+        q = __builtin_fma(q, u, BMFR_POWR_A1);
+        const double r = __builtin_fma(ep, u * q, ep);
+        const uint32_t low = (uint32_t)__double_as_longlong(r) & 0x1FFFFFFFu;
+        rare |= (uint32_t)(ok[c] && low - (0x10000000u - 1024u) < 2048u) << c;
+        out[c] = pos[c] ? (below[c] ? (float)r : 1.f) : 0.f;
+    }
+}
+
+__device__ __forceinline__ float gamma_clamped(float p, const double* tE = kPowrE, const double2* tRP = kPowrRP) {
+    bool rare;
+    const float v = gamma_table(p, rare, tE, tRP);
+    if (__builtin_expect(rare, 0)) return (float)__ocml_pow_f64((double)p, (double)0.454545f);
+    return v;
 }
 
 constexpr int kPowrENum = sizeof(kPowrE) / sizeof(double), kPowrRPNum = sizeof(kPowrRP) / sizeof(double2);

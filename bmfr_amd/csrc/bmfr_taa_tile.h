@@ -133,9 +133,14 @@ __device__ __forceinline__ void forward_reach(const TaaArgs& T, bool here = true
     }
 }
 
+#ifndef BMFR_K2_STRIP
+#define BMFR_K2_STRIP 1
+#endif
+constexpr bool kStrip = BMFR_K2_STRIP;
+
 // A tile's geometry: 64 x TH output pixels, NT threads (NT / 64 rows of 64
 // per pass, KN output pixels per thread), the tile and a 1-pixel ring in LDS.
-template <int TH, int NT>
+template <int TH, int NT, bool ST = false>
 struct TileShape {
     static constexpr int RP = NT / 64;  // tile rows per pass
     static_assert(TH % RP == 0 && TH >= RP, "tile height");
@@ -143,6 +148,12 @@ struct TileShape {
     static constexpr int RING = N - 64 * TH;  // halo pixels
     static constexpr int KN = TH / RP;        // output pixels per thread
     static_assert(RING <= NT, "one ring pixel per thread");
+    // Tile row of thread row ty's k-th output pixel: a strip of KN
+    // consecutive rows per thread (its KN 3x3 neighbourhoods overlap: one
+    // (KN + 2) x 3 window of LDS reads serves all of them), or with
+    // BMFR_K2_STRIP=0 rows ty, ty + RP, ... (a 3x3 read per pixel).  Either
+    // way a wave's loads and LDS accesses cover 64 consecutive pixels of a row.
+    static __device__ __forceinline__ int row(int ty, int k) { return ST ? ty * KN + k : ty + RP * k; }
 };
 
 // A thread's current-frame inputs of one tile, as loaded: the reprojected
@@ -170,21 +181,21 @@ __device__ __forceinline__ void ring_pixel(int t, int& hx, int& hy) {
 
 // Issue the tile's current-frame loads (reprojected positions first).  COH:
 // device-coherent loads of K1's outputs of the same launch.
-template <class IN, int TH, bool COH, int NT>
+template <class IN, int TH, bool COH, int NT, bool ST>
 __device__ __forceinline__ void tile_issue(const Params& P, const TaaArgs& T, int x0, int y0, int hx, int hy,
                                            TileLoads<IN, TileShape<TH, NT>::KN>& L) {
-    using S = TileShape<TH, NT>;
+    using S = TileShape<TH, NT, ST>;
     const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
     const CohPlane c_pp = coh_plane(T.prev_pixel), c_src = coh_plane(T.src);  // (unused unless COH)
 #pragma unroll
     for (int k = 0; k < S::KN; ++k) {
-        const uint32_t i = pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + ty + S::RP * k, P.ty1 - 1));
+        const uint32_t i = pix(P, min(x0 + tx, P.tx1 - 1), min(y0 + S::row(ty, k), P.ty1 - 1));
         if constexpr (COH) L.pf[k] = ld2_coh(c_pp, i);
         else L.pf[k] = ld_px(T.prev_pixel, i);
     }
 #pragma unroll
     for (int k = 0; k <= S::KN; ++k) {
-        const int lx = k < S::KN ? tx + 1 : hx, ly = k < S::KN ? ty + S::RP * k + 1 : hy;
+        const int lx = k < S::KN ? tx + 1 : hx, ly = k < S::KN ? S::row(ty, k) + 1 : hy;
         if (k == S::KN && t >= S::RING) break;
         // Clamped into the buffer region (= the image when untiled): a tile
         // whose last 64-px column or TH-row band overhangs its output reads
@@ -198,25 +209,58 @@ __device__ __forceinline__ void tile_issue(const Params& P, const TaaArgs& T, in
 
 // Tone map (bmfr.cl:851-856) of the loaded colours into the LDS window Y as
 // YCoCg; me[k]: this thread's own output pixels, tone-mapped RGB.
-template <class IN, int TH, int NT>
+template <class IN, int TH, int NT, bool ST>
 __device__ __forceinline__ void tile_tone(const Params& P, const TileLoads<IN, TileShape<TH, NT>::KN>& L, int hx,
                                           int hy, float4* __restrict__ Y, const double* __restrict__ sE,
                                           const double2* __restrict__ sRP, f3 (&me)[TileShape<TH, NT>::KN]) {
-    using S = TileShape<TH, NT>;
+    using S = TileShape<TH, NT, ST>;
     const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
-#pragma unroll
-    for (int k = 0; k <= S::KN; ++k) {
-        if (k == S::KN && t >= S::RING) break;
-        const int lx = k < S::KN ? tx + 1 : hx, ly = k < S::KN ? ty + S::RP * k + 1 : hy;
-#ifdef BMFR_PROBE_K2_NOTONE  // timing probe (wrong results): no tone map
-        const f3 a = widen(L.al[k]);
-        const f3 v{L.v[k].x * a.x, L.v[k].y * a.y, L.v[k].z * a.z};
-#else
-        const f3 v = tone_map(P, widen(L.al[k]), L.v[k], sE, sRP);
-#endif
+    // The correctly rounded powr's table part for every channel of every
+    // pixel, branch-free (gamma_table), so the compiler can issue a pixel's
+    // six table lookups together and overlap pixels; the rare values next to
+    // a float rounding midpoint (about one in 2^18) are redone afterwards
+    // through the whole tone map (gamma_clamped's fallback).  library_powr
+    // (uniform): the device library's powr, no fallback needed.
+    uint32_t rare = 0;  // bit k: a channel of pixel k needs the fallback
+    auto put = [&](int k, const f3& v) {
+        const int lx = k < S::KN ? tx + 1 : hx, ly = k < S::KN ? S::row(ty, k) + 1 : hy;
         if (k < S::KN) me[k] = v;
         const f3 yc = rgb_to_ycocg(v);
         Y[ly * S::HW + lx] = make_float4(yc.x, yc.y, yc.z, 0.f);
+    };
+#ifdef BMFR_PROBE_K2_NOTONE  // timing probe (wrong results): no tone map
+#pragma unroll
+    for (int k = 0; k <= S::KN; ++k) {
+        if (k == S::KN && t >= S::RING) break;
+        const f3 a = widen(L.al[k]);
+        put(k, f3{L.v[k].x * a.x, L.v[k].y * a.y, L.v[k].z * a.z});
+    }
+#else
+    if (P.library_powr) {
+#pragma unroll
+        for (int k = 0; k <= S::KN; ++k) {
+            if (k == S::KN && t >= S::RING) break;
+            put(k, tone_map(P, widen(L.al[k]), L.v[k], sE, sRP));
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k <= S::KN; ++k) {
+            if (k == S::KN && t >= S::RING) break;
+            // tone_map's arithmetic (bmfr.cl:851-856), the powr by table
+            const f3 a = widen(L.al[k]);
+            const float p[3] = {a.x * L.v[k].x, a.y * L.v[k].y, a.z * L.v[k].z};
+            float g[3];
+            uint32_t r;
+            gamma_table3(p, g, r, sE, sRP);
+            rare |= (r != 0 ? 1u : 0u) << k;
+            put(k, f3{g[0], g[1], g[2]});
+        }
+    }
+#endif
+    if (__builtin_expect(rare != 0, 0)) {
+#pragma unroll
+        for (int k = 0; k <= S::KN; ++k)
+            if (rare & (1u << k)) put(k, tone_map(P, widen(L.al[k]), L.v[k], sE, sRP));
     }
 }
 
@@ -235,23 +279,101 @@ __device__ __forceinline__ void tile_taps(const Params& P, const TaaArgs& T, con
     }
 }
 
+// Strip form of the resolve (kStrip): the thread's KN output pixels are KN
+// consecutive rows of one column, so their 3x3 neighbourhoods lie in one
+// (KN + 2) x 3 window.  Each window row is read from LDS once and reduced to
+// its box bounds (min / max of its three values) and its centre value; a
+// pixel's box bounds are then the bounds of its three rows' and its cross
+// bounds those of the top and bottom centres and the middle row -- the
+// sets of bmfr.cl:897-920, grouped differently (exact: taa_clamp_tail).
+// CHECK (tiles at the image border): out-of-image neighbours enter as +inf /
+// -inf, as in taa_clamp.
+template <int TH, int NT, bool CHECK>
+__device__ __forceinline__ void resolve_strip(const Params& P, const TaaArgs& T, int x0, int y0,
+                                              const float4* __restrict__ Y, const f3 (&me)[TileShape<TH, NT>::KN],
+                                              const float2 (&pf)[TileShape<TH, NT>::KN],
+                                              const f3 (&hist)[TileShape<TH, NT>::KN]) {
+    using S = TileShape<TH, NT, true>;
+    const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
+    const int r0 = S::row(ty, 0);  // the window's first row is tile row r0 - 1
+    struct Row {
+        f3 mn, mx;    // box bounds of the row's three neighbours
+        f3 clo, chi;  // its centre (as a lower / upper bound: +-inf when out of the image)
+    };
+    auto reduce_row = [&](int r) {
+        f3 lo[3], hi[3];
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+            const float4 q = Y[(r0 + r) * S::HW + tx + dx];
+            lo[dx] = hi[dx] = f3{q.x, q.y, q.z};
+            if constexpr (CHECK) {
+                const int sx = x0 + tx + dx - 1, sy = y0 + r0 + r - 1;
+                const bool in = sx >= 0 && sy >= 0 && sx < P.width && sy < P.height;
+                lo[dx] = in ? lo[dx] : f3{INFINITY, INFINITY, INFINITY};
+                hi[dx] = in ? hi[dx] : f3{-INFINITY, -INFINITY, -INFINITY};
+            }
+        }
+        Row w;
+        w.mn = f3{vmin3(lo[0].x, lo[1].x, lo[2].x), vmin3(lo[0].y, lo[1].y, lo[2].y), vmin3(lo[0].z, lo[1].z, lo[2].z)};
+        w.mx = f3{vmax3(hi[0].x, hi[1].x, hi[2].x), vmax3(hi[0].y, hi[1].y, hi[2].y), vmax3(hi[0].z, hi[1].z, hi[2].z)};
+        w.clo = lo[1];
+        w.chi = hi[1];
+        return w;
+    };
+    // min(+inf, a, b, c) / max(-inf, a, b, c): upstream's sets start from +-inf
+    auto mn4 = [](float a, float b, float c) { return vmin(vmin3s(INFINITY, a, b), c); };
+    auto mx4 = [](float a, float b, float c) { return vmax(vmax3s(-INFINITY, a, b), c); };
+    Row w0 = reduce_row(0), w1 = reduce_row(1);
+#pragma unroll
+    for (int k = 0; k < S::KN; ++k) {
+        const Row w2 = reduce_row(k + 2);
+        const int x = x0 + tx, y = y0 + r0 + k;
+        if (x < P.tx1 && y < P.ty1) {
+#ifdef BMFR_PROBE_K2_NORESOLVE  // timing probe (wrong results): no TAA resolve
+            const f3 r{me[k].x + w1.mn.x + hist[k].x, me[k].y + w1.mx.y + hist[k].y, me[k].z + w2.clo.z};
+#else
+            f3 r = me[k];
+            if (!taa_offscreen(P, pf[k], T.frame)) {
+                const f3 mnb{mn4(w0.mn.x, w1.mn.x, w2.mn.x), mn4(w0.mn.y, w1.mn.y, w2.mn.y),
+                             mn4(w0.mn.z, w1.mn.z, w2.mn.z)};
+                const f3 mxb{mx4(w0.mx.x, w1.mx.x, w2.mx.x), mx4(w0.mx.y, w1.mx.y, w2.mx.y),
+                             mx4(w0.mx.z, w1.mx.z, w2.mx.z)};
+                const f3 mnc{mn4(w0.clo.x, w1.mn.x, w2.clo.x), mn4(w0.clo.y, w1.mn.y, w2.clo.y),
+                             mn4(w0.clo.z, w1.mn.z, w2.clo.z)};
+                const f3 mxc{mx4(w0.chi.x, w1.mx.x, w2.chi.x), mx4(w0.chi.y, w1.mx.y, w2.chi.y),
+                             mx4(w0.chi.z, w1.mx.z, w2.chi.z)};
+                r = taa_clamp_tail(P, me[k], mnb, mxb, mnc, mxc, hist[k]);
+            }
+#endif
+            st3(T.result, pix(P, x, y), r);
+        }
+        w0 = w1;
+        w1 = w2;
+    }
+}
+
 // The resolve of the tile's output pixels from the complete window Y
 // (bmfr.cl:897-973) and the stores.
-template <int TH, int NT>
+template <int TH, int NT, bool ST>
 __device__ __forceinline__ void tile_resolve(const Params& P, const TaaArgs& T, int x0, int y0,
                                              const float4* __restrict__ Y, const f3 (&me)[TileShape<TH, NT>::KN],
                                              const float2 (&pf)[TileShape<TH, NT>::KN],
                                              const f3 (&hist)[TileShape<TH, NT>::KN]) {
-    using S = TileShape<TH, NT>;
+    using S = TileShape<TH, NT, ST>;
     const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
     // Tiles that reach the image border check every neighbour (bmfr.cl:901);
     // the others have all nine in the image.
     const bool edge = x0 == 0 || y0 == 0 || x0 + 64 >= P.width || y0 + TH >= P.height;
+    if constexpr (ST) {
+        if (edge) resolve_strip<TH, NT, true>(P, T, x0, y0, Y, me, pf, hist);
+        else resolve_strip<TH, NT, false>(P, T, x0, y0, Y, me, pf, hist);
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < S::KN; ++k) {
-        const int x = x0 + tx, y = y0 + ty + S::RP * k;
+        const int x = x0 + tx, y = y0 + S::row(ty, k);
         if (x < P.tx1 && y < P.ty1) {
-            const int c = (ty + S::RP * k + 1) * S::HW + tx + 1;
+            const int c = (S::row(ty, k) + 1) * S::HW + tx + 1;
             f3 nb[9];
 #pragma unroll
             for (int j = 0; j < 9; ++j) {
@@ -279,7 +401,7 @@ __device__ __forceinline__ void tile_resolve(const Params& P, const TaaArgs& T, 
 // taps (their latency under the barrier), each pixel's history as its taps
 // arrive (three values live instead of twelve: 89 VGPRs, five waves per
 // SIMD, where taps issued before the tone map held 124), the resolve.
-template <class IN, int TH, bool COH = false, int NT = 256>
+template <class IN, int TH, bool COH = false, int NT = 256, bool ST = false>
 __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int x0, int y0, float4* __restrict__ Y,
                                          double* __restrict__ sE, double2* __restrict__ sRP) {
     using S = TileShape<TH, NT>;
@@ -290,17 +412,17 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
     int hx = 0, hy = 0;
     ring_pixel<TH, NT>(t, hx, hy);
     TileLoads<IN, KN> L;
-    tile_issue<IN, TH, COH, NT>(P, T, x0, y0, hx, hy, L);
+    tile_issue<IN, TH, COH, NT, ST>(P, T, x0, y0, hx, hy, L);
     __syncthreads();  // the powr tables are in LDS
     f3 me[KN];
-    tile_tone<IN, TH, NT>(P, L, hx, hy, Y, sE, sRP, me);
+    tile_tone<IN, TH, NT, ST>(P, L, hx, hy, Y, sE, sRP, me);
     f3 taps[KN][4];
     tile_taps<KN>(P, T, L.pf, taps);
     __syncthreads();  // the window is complete
     f3 hist[KN];
 #pragma unroll
     for (int k = 0; k < KN; ++k) hist[k] = taa_history(P, L.pf[k], taps[k]);
-    tile_resolve<TH, NT>(P, T, x0, y0, Y, me, L.pf, hist);
+    tile_resolve<TH, NT, ST>(P, T, x0, y0, Y, me, L.pf, hist);
 }
 
 // The TAA part of a one-launch frame kernel (K1 blocks, then the frame's
@@ -324,7 +446,7 @@ __device__ __forceinline__ void frame_taa_part(const Params& P2, const TaaArgs& 
     constexpr int TH = frame_taa_h<NT>();
     const int gx = (P2.tx1 - P2.tx0 + 63) / 64, n2 = (int)gridDim.x - nk1p;
     const int gi = xcd_swizzle(b - nk1p, n2);
-    taa_tile<IN, TH, COH, NT>(P2, T, P2.tx0 + (gi % gx) * 64, P2.ty0 + (gi / gx) * TH, L.Y, L.sE, L.sRP);
+    taa_tile<IN, TH, COH, NT, kStrip>(P2, T, P2.tx0 + (gi % gx) * 64, P2.ty0 + (gi / gx) * TH, L.Y, L.sE, L.sRP);
     if constexpr (COH) {
         if (T.reach_dev && b == (int)gridDim.x - 1) {
             wait_all_k1_blocks(P2, T);
