@@ -16,7 +16,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libbmfr.so")
 DIAG_LIB = os.path.join(HERE, "libbmfr_diag.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["bmfr_kernels.hip", "bmfr_fused.hip", "bmfr_fused_cols.hip", "bmfr_capi.hip", "bmfr_exchange.hip",
+SOURCES = ["bmfr_kernels.hip", "bmfr_fused.hip", "bmfr_fused_cols.hip", "bmfr_fused_cols_f32.hip", "bmfr_capi.hip",
+           "bmfr_exchange.hip",
            "bmfr_synth.hip",
            "bmfr_generic_ns1.hip", "bmfr_generic_ns2.hip", "bmfr_generic_ns3.hip", "bmfr_generic_ns4.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize",

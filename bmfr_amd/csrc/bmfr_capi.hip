@@ -355,11 +355,7 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
     const size_t px = (size_t)sz.region_width * sz.region_height;  // every plane covers the region
     hipError_t e = hipSuccess;
     for (int i = 0; i < 2 && e == hipSuccess; ++i) {
-#ifdef BMFR_PROBE_K1_REC16
-        e = hipMalloc(&c->noisy_acc[i], px * 4 * sizeof(float));
-#else
         e = hipMalloc(&c->noisy_acc[i], px * 3 * sizeof(float));
-#endif
         if (e == hipSuccess) e = hipMalloc(&c->spp[i], px);
         if (e == hipSuccess) e = hipMalloc(&c->acc[i], px * 3 * sizeof(float));
         if (e == hipSuccess) e = hipMalloc(&c->result[i], px * 3 * sizeof(float));

@@ -30,6 +30,20 @@ struct __attribute__((packed, aligned(4))) f3mem {
     float x, y, z;
 };
 
+// Byte offsets of pixel i in planes of 12- and 6-byte elements: i * 3 as one
+// shift-and-add, then a shift -- two full-rate instructions, where the
+// compiler turns i * 12 into v_mul_lo_u32 (a multi-pass integer multiply).
+// i may reach 2^25 (8K frames), so a 24-bit multiply cannot do it.  Inline
+// asm so the shift-and-add is not folded back into a multiply; it reads and
+// writes plain integer VGPRs (no DOT / transcendental producer involved).
+__device__ __forceinline__ uint32_t times3(uint32_t i) {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 1, %1" : "=v"(r) : "v"(i));
+    return r;
+}
+__device__ __forceinline__ uint32_t x12(uint32_t i) { return times3(i) << 2; }
+__device__ __forceinline__ uint32_t x6(uint32_t i) { return times3(i) << 1; }
+
 // Device-coherent plane accesses, for data one work-group of a launch hands
 // to another that may run on another XCD (each XCD's L2 is write-back and
 // not coherent with the others'): raw buffer loads / stores with the sc1
@@ -45,13 +59,13 @@ constexpr int kSc1 = 0;  // timing probe only (tools/ab.py variants): plain hand
 constexpr int kSc1 = 16;  // buffer instruction cache-policy bit SC1
 #endif
 __device__ __forceinline__ f3 ld3_coh(CohPlane r, uint32_t i) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, i * 12u, 0, kSc1);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, x12(i), 0, kSc1);
     return f3{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2])};
 }
 __device__ __forceinline__ void st3_coh(CohPlane r, uint32_t i, f3 v) {
     typedef unsigned u3 __attribute__((ext_vector_type(3)));
     __builtin_amdgcn_raw_buffer_store_b96(u3{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z)}, r,
-                                          i * 12u, 0, kSc1);
+                                          x12(i), 0, kSc1);
 }
 __device__ __forceinline__ float2 ld2_coh(CohPlane r, uint32_t i) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, i * 8u, 0, kSc1);
@@ -80,7 +94,7 @@ template <int AUX = 0>
 __device__ __forceinline__ void st3_drop(DropPlane r, uint32_t i, bool keep, f3 v) {
     typedef unsigned u3 __attribute__((ext_vector_type(3)));
     __builtin_amdgcn_raw_buffer_store_b96(u3{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z)}, r,
-                                          keep ? i * 12u : kDropOff, 0, AUX);
+                                          keep ? x12(i) : kDropOff, 0, AUX);
 }
 template <int AUX = 0>
 __device__ __forceinline__ void st2_drop(DropPlane r, uint32_t i, bool keep, float2 v) {
@@ -116,11 +130,11 @@ __device__ __forceinline__ void st_px(T* b, uint32_t i, T v) {
     *at_byte(b, i * (uint32_t)sizeof(T)) = v;
 }
 __device__ __forceinline__ f3 ld3(const float* __restrict__ b, uint32_t i) {
-    const f3mem v = *reinterpret_cast<const f3mem*>(at_byte(b, i * 12u));
+    const f3mem v = *reinterpret_cast<const f3mem*>(at_byte(b, x12(i)));
     return f3{v.x, v.y, v.z};
 }
 __device__ __forceinline__ void st3(float* __restrict__ b, uint32_t i, f3 v) {
-    *reinterpret_cast<f3mem*>(at_byte(b, i * 12u)) = f3mem{v.x, v.y, v.z};
+    *reinterpret_cast<f3mem*>(at_byte(b, x12(i))) = f3mem{v.x, v.y, v.z};
 }
 
 // One pixel of an input plane of element type IN (float: the reference's
@@ -131,7 +145,7 @@ struct __attribute__((packed, aligned(2))) h3mem {
 template <class IN>
 __device__ __forceinline__ f3 ld3in(const float* __restrict__ b, uint32_t i) {
     if constexpr (sizeof(IN) == 2) {
-        const h3mem v = *reinterpret_cast<const h3mem*>(at_byte(b, i * 6u));
+        const h3mem v = *reinterpret_cast<const h3mem*>(at_byte(b, x6(i)));
         return f3{(float)v.x, (float)v.y, (float)v.z};
     } else {
         return ld3(b, i);
@@ -156,7 +170,7 @@ struct In3<_Float16> {
 };
 template <class IN>
 __device__ __forceinline__ In3<IN> ld3raw(const float* __restrict__ b, uint32_t i) {
-    if constexpr (sizeof(IN) == 2) return In3<IN>{*reinterpret_cast<const h3raw*>(at_byte(b, i * 6u))};
+    if constexpr (sizeof(IN) == 2) return In3<IN>{*reinterpret_cast<const h3raw*>(at_byte(b, x6(i)))};
     else return In3<IN>{ld3(b, i)};
 }
 __device__ __forceinline__ f3 widen(const In3<float>& r) { return r.v; }

@@ -1,5 +1,6 @@
 // bmfr_fused_cols.hip -- fused frame kernel K1, column-split form (default for
-// the canonical feature lists with half tmp_data).
+// the canonical feature lists with half tmp_data, and with f32 tmp_data under
+// fast_fit).
 //
 // Same computation as k_fused (bmfr_fused.hip): accumulate_noisy_data ->
 // min/max scaling -> Householder QR -> back substitution -> weighted_sum ->
@@ -25,6 +26,7 @@
 //
 // The R matrix, back substitution and phase-3 code are k_fused's.  Parity:
 // tests/test_gpu_parity.py (fused vs stage kernels bit for bit).
+#include <type_traits>
 #include <utility>
 
 #include "bmfr_launch.h"
@@ -54,20 +56,33 @@ constexpr int kUBufs = 3;
 // columns and then go there, so the work-group's LDS stays within 40 KB (four
 // work-groups per CU); otherwise they have their own LDS array.
 constexpr int kKeep = 16 * 3 * 64;  // 12 floats per thread at NW = 4, 6 at NW = 8
-constexpr bool keep_in_m(int B) {
-    return (B - 1) * 64 * kSlots * 2 >= (kUBufs * 64 * kUStride + kKeep) * 4;
+// F32: f32 tmp_data (USE_HALF_PRECISION_IN_TMP_DATA 0): the design matrix as
+// floats -- twice the registers per column (16 per lane, as 8 float pairs),
+// the trailing columns never rounded to half.  Only the rows another wave
+// needs pass through LDS: wave w computes row quad w of every column in
+// phase 1, and the quad of the columns it owns in the fit stays in its
+// registers, so LDS holds 12 of each lane's 16 rows (36 KB at B = 13: four
+// work-groups per CU, as with half tmp_data; all 16 would be 48 KB, three).
+template <bool F32>
+constexpr int m_slots() { return F32 ? kSlots - 4 : kSlots; }
+constexpr bool keep_in_m(int B, bool F32 = false) {
+    return (B - 1) * 64 * (F32 ? 4 * m_slots<true>() : 2 * kSlots) >= (kUBufs * 64 * kUStride + kKeep) * 4;
 }
-template <int B, int NW = 4>
+template <int B, int NW = 4, bool F32 = false>
 struct Lds {
+    using MT = std::conditional_t<F32, float, _Float16>;
     union {
-        _Float16 M[B - 1][64 * kSlots];  // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
+        // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
+        // (half pairs swizzled by lane, see run()); F32: [lane * 12 + 4 q' + j % 4],
+        // q' the row quad j / 4 among the three its owner wave does not hold
+        MT M[B - 1][64 * m_slots<F32>()];
         struct {
             float u[kUBufs][64 * kUStride];  // Householder vectors, u_c in buffer c % kUBufs
-            float keep_m[keep_in_m(B) ? kKeep : 1];
+            float keep_m[keep_in_m(B, F32) ? kKeep : 1];
         };
     };
-    float keep_s[keep_in_m(B) ? 1 : kKeep];
-    __device__ float* keep() { return keep_in_m(B) ? keep_m : keep_s; }  // [(item * 3 + ch) * 64 NW + t]
+    float keep_s[keep_in_m(B, F32) ? 1 : kKeep];
+    __device__ float* keep() { return keep_in_m(B, F32) ? keep_m : keep_s; }  // [(item * 3 + ch) * 64 NW + t]
     float piv[kUBufs][3];               // |u|^2 and RN(1/|u|^2) of the published vector; fast_fit: u's pivot element
     int pub;                            // highest published pivot column
     int prog[NW];                       // per wave: the last step it has applied
@@ -91,7 +106,18 @@ __device__ __forceinline__ void sfor(F&& f) {
     sfor_impl(std::make_integer_sequence<int, N>{}, f);
 }
 
-__device__ __forceinline__ float hget(const h2 (&a)[8], int j) { return (float)a[j >> 1][j & 1]; }
+typedef float f2v __attribute__((ext_vector_type(2)));
+// A column of the design matrix in one lane: rows l + 64 j, j = 0..15, as 8
+// pairs (2k, 2k + 1) -- packed halves (h2) or floats (f2v, F32).
+template <bool F32>
+using Pair = std::conditional_t<F32, f2v, h2>;
+template <class P2>
+__device__ __forceinline__ float hget(const P2 (&a)[8], int j) { return (float)a[j >> 1][j & 1]; }
+template <class P2>
+__device__ __forceinline__ void hset(P2 (&a)[8], int j, float v) {
+    if constexpr (std::is_same_v<P2, h2>) a[j >> 1][j & 1] = (_Float16)v;  // vstore_half, round to nearest even
+    else a[j >> 1][j & 1] = v;
+}
 
 __device__ __forceinline__ float lane_value(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
@@ -126,7 +152,6 @@ __device__ __forceinline__ float sub_h(h2 h, float q) {
 // With the fast path, the division is a Markstein step on the shared
 // reciprocal (exact for these operand ranges, tests/test_markstein.py);
 // non-finite or extreme operands take IEEE division (uniform branch).
-typedef float f2v __attribute__((ext_vector_type(2)));
 // Upstream's per-element operations: the dot's four partial chains as fused
 // mixed-precision FMAs (exact products, below), the quotients as packed
 // Markstein steps, two rows per instruction (every lane of a packed op rounds
@@ -241,6 +266,72 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
     __builtin_amdgcn_sched_barrier(0);  // one column in flight: bounds the register footprint
 }
 
+// f32 tmp_data (F32): the column update of step c >= 1 on float pairs.  The
+// dot's four partial chains are upstream's sums of rounded products
+// (bmfr.cl:608-617: tmp * u_vec, then +=) -- chains (0, 1) and (2, 3) as
+// packed pairs, every lane rounding as the scalar ops --, reduced in
+// upstream's association; then the update of bmfr.cl:646 as in
+// update_column (packed Markstein quotients, rows above the pivot kept) or,
+// with FAST (fast_fit: the fused update only, as the row-split f32 K1), one
+// fused multiply-add per element on RN(c2 / |u|^2).
+template <int c>
+__device__ __forceinline__ void update_column_f32(f2v (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
+                                                  int l, bool fast) {
+    f2v p01 = {0.f, 0.f}, p23 = {0.f, 0.f};
+#pragma unroll
+    for (int si = 0; si < 4; ++si) {
+        p01 = p01 + a[2 * si] * f2v{u[4 * si], u[4 * si + 1]};
+        p23 = p23 + a[2 * si + 1] * f2v{u[4 * si + 2], u[4 * si + 3]};
+        if (si == 0) p01.x = l >= c ? p01.x : 0.f;  // rows above the pivot: skipped
+    }
+    const float p[4] = {p01.x, p01.y, p23.x, p23.y};
+    const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);
+    if (fast) {  // wave-uniform
+        const float sc = c2 * recip;
+        const f2v vs = {sc, sc};
+        const float keep0 = a[0].x;
+#pragma unroll
+        for (int k = 0; k < kSlots / 2; ++k)
+            a[k] = __builtin_elementwise_fma(-f2v{u[2 * k], u[2 * k + 1]}, vs, a[k]);
+        a[0].x = l >= c ? a[0].x : keep0;  // rows above the pivot keep their value
+        __builtin_amdgcn_sched_barrier(0);
+        return;
+    }
+    f2v q[kSlots / 2];
+    if (fabsf(c2) < 0x1p100f && ulen2 >= 0x1p-100f && ulen2 < 0x1p100f) {
+        const f2v vb = {ulen2, ulen2}, vy = {recip, recip};
+#pragma unroll
+        for (int k = 0; k < kSlots / 2; ++k) {
+            const f2v av = f2v{u[2 * k], u[2 * k + 1]} * c2;
+            const f2v q0 = av * vy;
+            const f2v r = __builtin_elementwise_fma(-q0, vb, av);
+            q[k] = __builtin_elementwise_fma(r, vy, q0);
+        }
+    } else {
+        // Cold (never taken on finite data): IEEE division in a rolled loop
+        // rotating u and q by one pair (as update_column: no indexed arrays)
+        float uu[kSlots];
+#pragma unroll
+        for (int j = 0; j < kSlots; ++j) uu[j] = u[j];
+#pragma unroll 1
+        for (int k = 0; k < kSlots / 2; ++k) {
+            const f2v qk = {(uu[0] * c2) / ulen2, (uu[1] * c2) / ulen2};
+            const float u0 = uu[0], u1 = uu[1];
+#pragma unroll
+            for (int j = 0; j < kSlots - 2; ++j) uu[j] = uu[j + 2];
+            uu[kSlots - 2] = u0;
+            uu[kSlots - 1] = u1;
+#pragma unroll
+            for (int i = 0; i < kSlots / 2 - 1; ++i) q[i] = q[i + 1];
+            q[kSlots / 2 - 1] = qk;
+        }
+    }
+    q[0].x = l >= c ? q[0].x : 0.f;  // x - (+0) == x: rows above the pivot keep their value
+#pragma unroll
+    for (int k = 0; k < kSlots / 2; ++k) a[k] = a[k] - q[k];
+    __builtin_amdgcn_sched_barrier(0);  // one column in flight: bounds the register footprint
+}
+
 // Step 0: column 0 is FEATURE_BUFFERS[0] = 1.f, so u = (1 - 32, 1, 1, ...),
 // |u|^2 = 1984 and u*x = x exactly (see k_fused's qr_column<0>).  Noise is
 // added to feature columns on this first load (bmfr.cl:625-627).
@@ -249,8 +340,8 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
 // The table holds the float factors (rnd - 0.5f); the term is noise2 * factor
 // in double (bmfr.cl:173-182), formed here: 16 floats per lane -- one round
 // trip for the column's loads.
-template <bool FAST = false>
-__device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const float* __restrict__ noise,
+template <bool FAST = false, class P2>
+__device__ __forceinline__ void update_column0(P2 (&a)[8], int l, const float* __restrict__ noise,
                                                const float (&pre)[kSlots], bool use_pre, double noise2) {
     float x[kSlots];
 #pragma unroll
@@ -298,7 +389,7 @@ __device__ __forceinline__ void update_column0(h2 (&a)[8], int l, const float* _
     for (int j = 0; j < kSlots; ++j) nv[j] = x[j] - q;
     nv[0] = l == 0 ? x[0] - q0 : nv[0];
 #pragma unroll
-    for (int j = 0; j < kSlots; ++j) a[j >> 1][j & 1] = (_Float16)nv[j];
+    for (int j = 0; j < kSlots; ++j) hset(a, j, nv[j]);
     __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -322,26 +413,30 @@ __device__ __forceinline__ void wait_flag(LDS& L, const int* flag, int c) {
         if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= c) return;
     }
 }
-template <int B, int NW>
-__device__ __forceinline__ void wait_pub(Lds<B, NW>& L, int c) {
+template <class LDS>
+__device__ __forceinline__ void wait_pub(LDS& L, int c) {
     wait_flag(L, &L.pub, c);
 }
-template <int B, int NW>
-__device__ __forceinline__ void wait_all_progress(Lds<B, NW>& L, int c) {
+template <int NW, class LDS>
+__device__ __forceinline__ void wait_all_progress(LDS& L, int c) {
     for (int w = 0; w < NW; ++w) wait_flag(L, &L.prog[w], c);
 }
 
 // The owner of pivot column c (>= 1), once steps 0..c-1 are applied to it:
 // |x|^2 over rows >= c+1, the Householder vector u and |u|^2 (bmfr.cl:555-601),
-// published to LDS with the R column.
-template <int c, int B, int NW, bool FAST = false>
-__device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B, NW>& L, int l) {
+// published to LDS with the R column.  FAST (half tmp_data only): hardware
+// sqrt / reciprocal, butterfly sum, u published as the column's halves.
+template <int c, int B, int NW, bool FAST = false, class P2, class LDS>
+__device__ __forceinline__ void publish_pivot(const P2 (&a)[8], LDS& L, int l) {
     constexpr int RE = B - 2;
+    constexpr bool F32 = std::is_same_v<P2, f2v>;
+    static_assert(!(FAST && F32), "f32 tmp_data publishes f32 pivots");
     float x[kSlots];
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
     // |x|^2 over rows >= c + 1 (bmfr.cl:555-569): squares of halves are
-    // exact, so the fused square-and-add chains are upstream's sums bit for bit.
+    // exact, so the fused square-and-add chains are upstream's sums bit for
+    // bit; f32 squares are rounded, then added (upstream's strict sequence).
     float p[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -350,7 +445,8 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B, NW>& L, i
         for (int si = 0; si < 4; ++si) {
             const int j = m + 4 * si;
             const float xj = j == 0 && l < c + 1 ? 0.f : x[j];
-            s = __builtin_fmaf(xj, xj, s);
+            if constexpr (F32) s = s + xj * xj;
+            else s = __builtin_fmaf(xj, xj, s);
         }
         p[m] = s;
     }
@@ -363,7 +459,7 @@ __device__ __forceinline__ void publish_pivot(const h2 (&a)[8], Lds<B, NW>& L, i
     const float ulen2 = sumsq + ucl2 * ucl2;
     if (l == c) x[0] = ucl2;
     constexpr int buf = c % kUBufs;
-    if constexpr (c >= kUBufs) wait_all_progress(L, c - kUBufs);  // readers of u_{c-3} done
+    if constexpr (c >= kUBufs) wait_all_progress<NW>(L, c - kUBufs);  // readers of u_{c-3} done
     if constexpr (FAST) {  // u as the column's halves, rows <= c zeroed; the pivot element in piv[2]
         uint32_t w[8];
 #pragma unroll
@@ -403,13 +499,18 @@ __device__ __forceinline__ void k1_barrier() { lds_barrier(); }
 // implicit.  W is a run-time (wave-uniform) value, so the NW waves run one
 // copy of the code: column ownership is a scalar branch, while the slot of
 // every column a step touches is known at compile time.
-template <int NS, int FS, int NW = 4, bool FAST = false>
+template <int NS, int FS, int NW = 4, bool FAST = false, bool F32 = false>
 struct WaveFit {
     static constexpr int B = NS + FS + 3;
+    // fast_fit: the fused trailing update (FAST); with half tmp_data also the
+    // butterfly reductions, f32 noise add and hardware sqrt / reciprocals
+    // (FASTR) -- f32 tmp_data fuses the update only, as the row-split K1 did.
+    static constexpr bool FASTR = FAST && !F32;
+    using P2 = Pair<F32>;
     static constexpr int NF = B - 3;  // pivot columns
     static constexpr int NSL = (B - 1 + NW - 1) / NW;
     static constexpr int NT = 64 * NW, NI = 16 / NW;  // threads, items (rows) per thread in phases 1 and 3
-    using LDS = Lds<B, NW>;
+    using LDS = Lds<B, NW, F32>;
     static __device__ __forceinline__ bool owns(int W, int c) { return c >= 1 && c < B && (c - 1) % NW == W; }
     static constexpr int owner(int c) { return (c - 1) % NW; }
     static constexpr int slot(int c) { return (c - 1) / NW; }
@@ -417,36 +518,37 @@ struct WaveFit {
     // feature column for every wave): none at B = 16 with four waves, where
     // the fit's registers are the limit for four work-groups per CU.
     static constexpr int NP = B >= 16 && NW == 4 ? 0 : ((NF - 1) / NW < kPre ? (NF - 1) / NW : kPre);
+    static_assert(!F32 || NW == 4, "f32 tmp_data: row quad w of wave w");
     static_assert(NP == 0 || NW * NP < NF, "prefetched slots hold feature columns");
 
     // The first column a wave updates at step 0: a feature column for every wave.
     static __device__ __forceinline__ int first_column(int W) { return 1 + W; }
 
     template <int c>
-    static __device__ __forceinline__ void step(h2 (&a)[NSL][8], LDS& L, int W, int l,
+    static __device__ __forceinline__ void step(P2 (&a)[NSL][8], LDS& L, int W, int l,
                                                 const float* __restrict__ noise, const float (&pre)[kPre][kSlots],
                                                 double noise2) {
         constexpr int nxt = c + 1;  // the next pivot column, slot(nxt) of wave owner(nxt)
         const bool publish = nxt < NF && W == owner(nxt);
         if constexpr (c == 0) {
             if (publish) {  // column 1 of wave 0: its first column
-                update_column0<FAST>(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre[0], NP > 0, noise2);
-                publish_pivot<nxt, B, NW, FAST>(a[slot(nxt)], L, l);
+                update_column0<FASTR>(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre[0], NP > 0, noise2);
+                publish_pivot<nxt, B, NW, FASTR>(a[slot(nxt)], L, l);
             }
             sfor<NSL>([&](auto K) {
                 constexpr int k = decltype(K)::value;
                 const int fb = 1 + W + NW * k;
                 if (owns(W, fb) && !(publish && fb == nxt))  // slots < NP: feature columns, prefetched
-                    update_column0<FAST>(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr,
+                    update_column0<FASTR>(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr,
                                    pre[k < kPre ? k : 0], k < NP, noise2);
             });
         } else {
             if (1 + W + NW * ((B - 2 - W) / NW) > c) {  // this wave's last column is past the pivot
                 wait_pub(L, c);
-                float u[FAST ? 1 : kSlots];
-                h2 uh[FAST ? 8 : 1];
+                float u[FASTR ? 1 : kSlots];
+                h2 uh[FASTR ? 8 : 1];
                 float uc = 0.f;
-                if constexpr (FAST) {
+                if constexpr (FASTR) {
                     const uint4* src = reinterpret_cast<const uint4*>(&L.u[c % kUBufs][l * kUStride]);
                     const uint4 v0 = src[0], v1 = src[1];
                     const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
@@ -465,14 +567,15 @@ struct WaveFit {
                     }
                 }
                 const float ulen2 = L.piv[c % kUBufs][0], recip = L.piv[c % kUBufs][1];
-                auto upd = [&](h2 (&col)[8]) {
-                    if constexpr (FAST) update_column_fast<c>(col, uh, uc, recip);
+                auto upd = [&](P2 (&col)[8]) {
+                    if constexpr (F32) update_column_f32<c>(col, u, ulen2, recip, l, FAST);
+                    else if constexpr (FAST) update_column_fast<c>(col, uh, uc, recip);
                     else update_column<c>(col, u, ulen2, recip, l);
                 };
                 if constexpr (nxt < NF) {
                     if (publish) {  // the next pivot is every wave's critical path: issue it first
                         upd(a[slot(nxt)]);
-                        publish_pivot<nxt, B, NW, FAST>(a[slot(nxt)], L, l);
+                        publish_pivot<nxt, B, NW, FASTR>(a[slot(nxt)], L, l);
                     }
                 }
                 sfor<NSL>([&](auto K) {
@@ -489,7 +592,7 @@ struct WaveFit {
     }
 
     template <int... C>
-    static __device__ __forceinline__ void steps(h2 (&a)[NSL][8], LDS& L, int W, int l,
+    static __device__ __forceinline__ void steps(P2 (&a)[NSL][8], LDS& L, int W, int l,
                                                  const float* __restrict__ noise, const float (&pre)[kPre][kSlots],
                                                  double noise2, std::integer_sequence<int, C...>) {
         (step<C>(a, L, W, l, noise, pre, noise2), ...);
@@ -511,17 +614,34 @@ struct WaveFit {
 
     static __device__ __forceinline__ void run(LDS& L, int W, int l, const float* __restrict__ noise,
                                                const float (&pre)[kPre][kSlots], double noise2, int mp,
-                                               const float (&kp)[NI][3]) {
-        h2 a[NSL][8];
+                                               const float (&kp)[NI][3], const f2v (&own)[NSL][2]) {
+        P2 a[NSL][8];
         sfor<NSL>([&](auto K) {
             constexpr int k = decltype(K)::value;
             const int c = 1 + W + NW * k;
             if (owns(W, c)) {
-                // pair p of lane l's row slot sits at dword p ^ ((l >> 2) & 7) (see phase 1)
-                const uint32_t* src = reinterpret_cast<const uint32_t*>(&L.M[c - 1][l * kSlots]);
-                const int q = (l >> 2) & 7;
+                if constexpr (F32) {
+                    // quad W from phase 1's registers, the others from LDS (a lane
+                    // stride of 12 floats: conflict-free 16-byte reads)
+                    const float4* src = reinterpret_cast<const float4*>(&L.M[c - 1][l * m_slots<true>()]);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) a[k][i] = __builtin_bit_cast(h2, src[i ^ q]);
+                    for (int i = 0; i < 4; ++i) {
+                        if (i == W) {
+                            a[k][2 * i] = own[k][0];
+                            a[k][2 * i + 1] = own[k][1];
+                        } else {
+                            const float4 v = src[i - (i > W)];
+                            a[k][2 * i] = f2v{v.x, v.y};
+                            a[k][2 * i + 1] = f2v{v.z, v.w};
+                        }
+                    }
+                } else {
+                    // pair p of lane l's row slot sits at dword p ^ ((l >> 2) & 7) (see phase 1)
+                    const uint32_t* src = reinterpret_cast<const uint32_t*>(&L.M[c - 1][l * kSlots]);
+                    const int q = (l >> 2) & 7;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) a[k][i] = __builtin_bit_cast(h2, src[i ^ q]);
+                }
             }
         });
         if (W == 0 && l < NW + 3) {  // read only after the barrier below
@@ -531,7 +651,7 @@ struct WaveFit {
             else L.prog[l - 1] = -1;
         }
         k1_barrier();  // the u buffers alias M
-        if constexpr (keep_in_m(B)) {  // phase 1's kept colours into the matrix area beside the u buffers
+        if constexpr (keep_in_m(B, F32)) {  // phase 1's kept colours into the matrix area beside the u buffers
             const int t = W * 64 + l;
 #pragma unroll
             for (int i = 0; i < NI; ++i)
@@ -556,8 +676,8 @@ struct WaveFit {
                         lo[m] = fminf(v, lo[m]);
                     }
                 }
-                const float bmax = wave_reduce<RedOp::Max, FAST>(hi);
-                const float bmin = wave_reduce<RedOp::Min, FAST>(lo);
+                const float bmax = wave_reduce<RedOp::Max, FASTR>(hi);
+                const float bmin = wave_reduce<RedOp::Min, FASTR>(lo);
                 const float d = bmax - bmin;
                 const bool divide = fabsf(d) > 1.0f;  // scale(), bmfr.cl:200-205
                 const float rcp = 1.f / d;
@@ -570,8 +690,8 @@ struct WaveFit {
                 for (int j = 0; j < kSlots; ++j) {
                     const float v = hget(a[k], j) - bmin;
                     // fast_fit: one multiply by the rounded reciprocal (as phase 3)
-                    const float sv = FAST ? v * rcp : div_by_recip(v, d, rcp);
-                    a[k][j >> 1][j & 1] = (_Float16)(divide ? sv : v);
+                    const float sv = FASTR ? v * rcp : div_by_recip(v, d, rcp);
+                    hset(a[k], j, divide ? sv : v);
                 }
             }
         });
@@ -610,8 +730,8 @@ template <int N>
 __device__ __forceinline__ float row_bcast(float v) {  // every lane <- lane N of its row
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + N, 0xf, 0xf, false));
 }
-template <int B, int NW>
-__device__ __forceinline__ void back_substitute_regs(Lds<B, NW>& L, int t) {
+template <int B, class LDS>
+__device__ __forceinline__ void back_substitute_regs(LDS& L, int t) {
     constexpr int RE = B - 2;
     static_assert(RE <= 16, "one DPP row per channel");
     if (t >= 64) return;
@@ -655,9 +775,11 @@ __device__ __forceinline__ void back_substitute_regs(Lds<B, NW>& L, int t) {
 // COH: the TAA tiles of the same frame run in this launch: the accumulated
 // colour and the reprojected positions they read are stored device-coherent
 // and the block publishes done[g] = epoch once they are.
-template <int NS, int FS, class IN, bool COH = false, int NW = 4, bool FAST = false>
-__device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, Lds<NS + FS + 3, NW>& L, int g) {
+template <int NS, int FS, class IN, bool COH = false, int NW = 4, bool FAST = false, bool F32 = false>
+__device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, Lds<NS + FS + 3, NW, F32>& L, int g) {
     constexpr int B = NS + FS + 3;
+    constexpr bool FASTR = FAST && !F32;  // WaveFit::FASTR
+    using P2 = Pair<F32>;
     constexpr int NT = 64 * NW, NI = 16 / NW;  // threads; items (rows) per thread
     const int t = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -689,7 +811,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // kInterleave with fast_fit: K1 -1.1 %; on the exact path +1.1 % (its
     // half-at-a-time matrix stores), so not there (profiles/r04_ab_row_interleave.txt).
 #ifndef BMFR_K1_INTERLEAVE
-#define BMFR_K1_INTERLEAVE (FAST ? 1 : 0)
+#define BMFR_K1_INTERLEAVE (FASTR ? 1 : 0)
 #endif
     // 0: own 8 rows; 1: slot NW i + w; 2: item pairs interleaved (slots 2 NW (i / 2) + 2 w + (i & 1):
     // a thread's two items of a pair stay adjacent slots, one 4-byte store per column)
@@ -702,7 +824,10 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     auto item_row = [&](int lane, int i) { return (lane >> 5) + 2 * item_slot(i); };
 
     // ---- accumulate_noisy_data (bmfr.cl:310-484), rows l + 64 (NI w + i) ----
-    h2 pk[B];            // features of an item pair, packed for one 4-byte LDS store per column
+    P2 pk[B];            // features of an item pair, packed for one LDS store per column
+    // F32: this wave's row quad of the columns it owns in the fit (slot k:
+    // column 1 + w + NW k), never stored to LDS
+    f2v own[WaveFit<NS, FS, NW, FAST, F32>::NSL][2];
     uint32_t spps = 0;   // per item i, bits 8i..8i+7: its new spp
     uint32_t ibits = 0;  // per item i, bit i: owner; bit 4 + i: accepted taps with weight > 0
     int over = 0;        // reprojection taps outside the valid state rectangle (tiled contexts)
@@ -716,7 +841,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // phase 3 (no second read of those planes: 24 B/px of f32 input; K1
     // -4 %); the exact fit (K1 +12 %, 84-96 bytes of spills) and B = 16
     // (76-144 bytes) hold too many registers for it.
-    constexpr bool kKeepNP = FAST && B < 16;
+    constexpr bool kKeepNP = FASTR && B < 16;
     In3<IN> keep_n[NI], keep_p[NI];
     NoisyCur<IN> cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + item_row(l, 0), frame);
 #pragma unroll
@@ -736,20 +861,24 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 float v;
                 if (f < B - 3) v = feature_value(f, it.n, it.p);
                 else v = f == B - 3 ? it.color.x : (f == B - 2 ? it.color.y : it.color.z);
-                // NaN -> 0 (bmfr.cl:468-469), then the +-65504 clamp (bmfr.cl:471-473)
-                // as one med3 (equal to fmax(fmin(v, 65504), -65504) for every non-NaN v)
-                v = __builtin_isnan(v) ? 0.0f : __builtin_amdgcn_fmed3f(v, -65504.f, 65504.f);
+                // NaN -> 0 (bmfr.cl:468-469), then (half tmp_data) the +-65504
+                // clamp (bmfr.cl:471-473) as one med3 (equal to fmax(fmin(v, 65504),
+                // -65504) for every non-NaN v)
+                if constexpr (F32) v = __builtin_isnan(v) ? 0.0f : v;
+                else v = __builtin_isnan(v) ? 0.0f : __builtin_amdgcn_fmed3f(v, -65504.f, 65504.f);
                 if constexpr (kInterleave) {  // this item's half of its row-slot pair (XOR-swizzled as below)
+                    static_assert(!F32, "f32 tmp_data stores item pairs");
                     const int j = item_slot(i);
                     L.M[f - 1][l * kSlots + 2 * ((j >> 1) ^ ((l >> 2) & 7)) + (j & 1)] = (_Float16)v;
                 } else {
-                    pk[f][i & 1] = (_Float16)v;
+                    if constexpr (F32) pk[f][i & 1] = v;
+                    else pk[f][i & 1] = (_Float16)v;
                 }
             }
             spps |= (uint32_t)it.spp << (8 * i);
             ibits |= ((uint32_t)it.owner << i) | ((uint32_t)it.prev_f_divided << (4 + i));
             over = max(over, it.over);
-            if constexpr (keep_in_m(B)) {
+            if constexpr (keep_in_m(B, F32)) {
                 kp[i][0] = it.prev_f.x;
                 kp[i][1] = it.prev_f.y;
                 kp[i][2] = it.prev_f.z;
@@ -759,40 +888,45 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 L.keep_s[(i * 3 + 2) * NT + t] = it.prev_f.z;
             }
             // owners only (bmfr.cl:478-484), as branch-free stores (st3_drop)
-#if defined(BMFR_PROBE_K1_REC16)
-            {
-                typedef unsigned u4 __attribute__((ext_vector_type(4)));
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    u4{__float_as_uint(it.color.x), __float_as_uint(it.color.y), __float_as_uint(it.color.z), it.spp},
-                    drop_plane(A.noisy_out), it.owner ? it.lin * 16u : kDropOff, 0, 0);
-            }
-#else
             st3_drop(drop_plane(A.noisy_out), it.lin, it.owner, it.color);
-#endif
-#if !defined(BMFR_PROBE_K1_REC) && !defined(BMFR_PROBE_K1_REC16)
             st1_drop(drop_plane(A.spp_out), it.lin, it.owner, it.spp);
-#endif
             st2_drop<COH ? kSc1 : 0>(drop_plane(A.prev_pixel_out), it.lin, it.owner, make_float2(it.pfx, it.pfy));
             if (!kInterleave && (i & 1)) {  // rows j = NI w + i - 1, NI w + i: adjacent halves of lane l's row slot
-                // (pair (NI w + i) / 2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)
-                const int pair = (item_slot(i) / 2) ^ ((l >> 2) & 7);
+                if constexpr (F32) {
+                    // rows 4 w + i - 1, 4 w + i: half (i - 1) / 2 of quad w; columns of
+                    // wave w stay in registers, the others go to compacted quad
+                    // w - (w > owner) of the owner's view (see Lds::M)
+                    static_assert(kIlv == 0, "f32 tmp_data: wave w computes row quad w");
 #pragma unroll
-                for (int f = 1; f < B; ++f)
-                    *reinterpret_cast<uint32_t*>(&L.M[f - 1][l * kSlots + 2 * pair]) = __builtin_bit_cast(uint32_t, pk[f]);
+                    for (int f = 1; f < B; ++f) {
+                        const int ow = (f - 1) % NW;
+                        if (w == ow) own[(f - 1) / NW][i >> 1] = pk[f];
+                        else
+                            *reinterpret_cast<f2v*>(&L.M[f - 1][l * m_slots<true>() + 4 * (w - (w > ow)) + (i - 1)]) =
+                                pk[f];
+                    }
+                } else {
+                    // (pair (NI w + i) / 2; XOR-swizzled by lane so a wave's 4-byte stores hit 32 banks)
+                    const int pair = (item_slot(i) / 2) ^ ((l >> 2) & 7);
+#pragma unroll
+                    for (int f = 1; f < B; ++f)
+                        *reinterpret_cast<uint32_t*>(&L.M[f - 1][l * kSlots + 2 * pair]) =
+                            __builtin_bit_cast(uint32_t, pk[f]);
+                }
             }
         }
         if (i < NI - 1) cur = nxt;
     }
     report_reach(P, A.reach, over);
     float pre[kPre][kSlots];
-    WaveFit<NS, FS, NW, FAST>::prefetch_noise(w, l, A.noise, pre);
+    WaveFit<NS, FS, NW, FAST, F32>::prefetch_noise(w, l, A.noise, pre);
     k1_barrier();  // matrix in LDS; phase 1's global stores drain in the background
     BMFR_STAMP(1);
     BMFR_STAMP(2);  // scaling runs inside the per-wave fit
 
     // ---- fit: min/max scaling, Householder QR, right-hand side ----
     if (t == 0) L.delay = P.debug_delay;  // read after the fit's barriers
-    WaveFit<NS, FS, NW, FAST>::run(L, w, l, A.noise, pre, P.noise2, P.max_polls, kp);
+    WaveFit<NS, FS, NW, FAST, F32>::run(L, w, l, A.noise, pre, P.noise2, P.max_polls, kp, own);
     // Phase 3's loads (normal and position of the NI items, bmfr.cl:725-729)
     // go out now: they land while wave 0 back-substitutes and the others wait.
     int l3 = l;  // opaque copy: recompute phase-1 addresses instead of keeping them live across the fit
@@ -871,7 +1005,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 f2v v = {feature_value(f, nrm[2 * h], wp[2 * h]), feature_value(f, nrm[2 * h + 1], wp[2 * h + 1])};
                 if (f >= NS) {
                     v = v - f2v{bmin, bmin};
-                    if (FAST) {
+                    if (FASTR) {
                         if (fabsf(d) > 1.0f) v = v * f2v{rcp, rcp};  // fast_fit: as the fit scaled it
                     } else if (fabsf(d) > 1.0f) {
                         const f2v q0 = v * f2v{rcp, rcp};
@@ -938,17 +1072,33 @@ constexpr int kNW = BMFR_K1_WAVES;
 constexpr int kK1Threads = 64 * kNW;
 // Minimum waves per SIMD for the register allocator: 4 work-groups of 4
 // waves per CU (128 VGPRs), or 3 of 8 (80); -DBMFR_K1_MIN_WAVES overrides.
+// f32 tmp_data: the compacted matrix's LDS allows four work-groups per CU at
+// B = 13 (38 KB each), three at B = 16 (48 KB); at B = 13 the exact fit
+// needs more than 128 VGPRs (78 spilled at four), so three there.
+#ifndef BMFR_F32_WAVES6
+#define BMFR_F32_WAVES6 4
+#endif
+#ifndef BMFR_F32_WAVES6X
+#define BMFR_F32_WAVES6X 3
+#endif
+#ifndef BMFR_F32_WAVES9
+#define BMFR_F32_WAVES9 3
+#endif
 #ifdef BMFR_K1_MIN_WAVES
 constexpr int kMinWavesSimd = BMFR_K1_MIN_WAVES;
 #else
 constexpr int kMinWavesSimd = kNW == 4 ? 4 : 6;
 #endif
+template <int FS, bool F32, bool FAST>
+constexpr int min_waves() {
+    return F32 ? (FS == 6 ? (FAST ? BMFR_F32_WAVES6 : BMFR_F32_WAVES6X) : BMFR_F32_WAVES9) : kMinWavesSimd;
+}
 
 // FAST: bmfr_config.fast_fit (the fused trailing update, update_column).
-template <int NS, int FS, class IN, bool FAST = false>
-__global__ __launch_bounds__(kK1Threads, kMinWavesSimd) void k_fused_cols(Params P, K1Args A) {
-    __shared__ Lds<NS + FS + 3, kNW> L;
-    k1_cols_body<NS, FS, IN, false, kNW, FAST>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
+template <int NS, int FS, class IN, bool FAST = false, bool F32 = false>
+__global__ __launch_bounds__(kK1Threads, (min_waves<FS, F32, FAST>())) void k_fused_cols(Params P, K1Args A) {
+    __shared__ Lds<NS + FS + 3, kNW, F32> L;
+    k1_cols_body<NS, FS, IN, false, kNW, FAST, F32>(P, A, L, xcd_swizzle(blockIdx.x, gridDim.x));
 }
 
 // K1 and K2 (64 x kFrameTaaH tiles) in one launch: work-groups [0, nk1) are K1
@@ -964,64 +1114,84 @@ __global__ __launch_bounds__(kK1Threads, kMinWavesSimd) void k_fused_cols(Params
 //     their outputs device-coherent.  Work-groups of one XCD are dispatched
 //     in order, so every K1 block a waiting tile needs has been dispatched:
 //     the waits end.
-template <int NS, int FS, class IN, bool SAME = false, bool FAST = false>
-__global__ __launch_bounds__(kK1Threads, kMinWavesSimd) void k_fused_cols_taa(Params P, K1Args A, Params P2,
-                                                                              TaaArgs T, int nk1, int nk1p) {
+template <int NS, int FS, class IN, bool SAME = false, bool FAST = false, bool F32 = false>
+__global__ __launch_bounds__(kK1Threads, (min_waves<FS, F32, FAST>())) void k_fused_cols_taa(Params P, K1Args A, Params P2,
+                                                                                    TaaArgs T, int nk1, int nk1p) {
     __shared__ union {
-        Lds<NS + FS + 3, kNW> k1;
+        Lds<NS + FS + 3, kNW, F32> k1;
         FrameTaaLds<kK1Threads> k2;
     } U;
     const int b = blockIdx.x;
-    if (b < nk1) k1_cols_body<NS, FS, IN, SAME, kNW, FAST>(P, A, U.k1, xcd_swizzle(b, nk1));
+    if (b < nk1) k1_cols_body<NS, FS, IN, SAME, kNW, FAST, F32>(P, A, U.k1, xcd_swizzle(b, nk1));
     else if (b >= nk1p) frame_taa_part<IN, SAME, kK1Threads>(P2, T, b, nk1p, U.k2);
 }
 
 }  // namespace cols
 
-bool fused_cols_supported(const Params& P) { return P.half_tmp && fused_supported(P); }
+// The column-split kernels of one tmp_data precision, compiled in their own
+// translation unit (bmfr_fused_cols_f32.hip includes this file with
+// BMFR_COLS_F32 = 1): K1 alone, the one-launch frame, the sequence launch.
+template <bool F32>
+hipError_t launch_cols_k1(const Params& P, hipStream_t st, const FusedArgs& A);
+template <bool F32>
+hipError_t launch_cols_frame_one(const Params& P, hipStream_t st, const FusedArgs& A);
+template <bool F32>
+hipError_t launch_cols_k1_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
+                              const FusedArgs* A2);
+
+#ifndef BMFR_COLS_F32
+#define BMFR_COLS_F32 0
+#endif
+constexpr bool kColsF32 = BMFR_COLS_F32;
+
+// The launchers below differ between the two translation units (kColsF32)
+// under the same names: internal linkage, or the linker keeps one TU's copy
+// of each inline go() for both.
+namespace {
 
 // The column-split kernels' template arguments from the run-time parameters:
 // FS (6 or 9 scaled features), the input element type, fast_fit.
+// f32 tmp_data runs the exact fit row-split (bmfr_fused.hip: K1 -4 % against
+// the column split's, whose exact fit needs 145 VGPRs, three waves per SIMD)
+// unless -DBMFR_F32_COLS_EXACT=1; fast_fit column-split (K1 -8 %).
+#ifndef BMFR_F32_COLS_EXACT
+#define BMFR_F32_COLS_EXACT 0
+#endif
+constexpr bool kColsExact = !kColsF32 || BMFR_F32_COLS_EXACT;
+
 template <template <int, class, bool> class L, class... Args>
-static void dispatch_cols(const Params& Q, Args&&... args) {
-    if (Q.scaled == 6) {
-        if (Q.input_half) Q.fast_fit ? L<6, _Float16, true>::go(args...) : L<6, _Float16, false>::go(args...);
-        else Q.fast_fit ? L<6, float, true>::go(args...) : L<6, float, false>::go(args...);
-    } else {
-        if (Q.input_half) Q.fast_fit ? L<9, _Float16, true>::go(args...) : L<9, _Float16, false>::go(args...);
-        else Q.fast_fit ? L<9, float, true>::go(args...) : L<9, float, false>::go(args...);
+void dispatch_cols(const Params& Q, Args&&... args) {
+    if constexpr (kColsExact) {
+        if (Q.scaled == 6) {
+            if (Q.input_half) Q.fast_fit ? L<6, _Float16, true>::go(args...) : L<6, _Float16, false>::go(args...);
+            else Q.fast_fit ? L<6, float, true>::go(args...) : L<6, float, false>::go(args...);
+        } else {
+            if (Q.input_half) Q.fast_fit ? L<9, _Float16, true>::go(args...) : L<9, _Float16, false>::go(args...);
+            else Q.fast_fit ? L<9, float, true>::go(args...) : L<9, float, false>::go(args...);
+        }
+    } else {  // callers check fused_cols_supported
+        if (Q.scaled == 6) Q.input_half ? L<6, _Float16, true>::go(args...) : L<6, float, true>::go(args...);
+        else Q.input_half ? L<9, _Float16, true>::go(args...) : L<9, float, true>::go(args...);
     }
 }
 
 template <int FS, class IN, bool FAST>
 struct LaunchCols {
     static void go(const Params& P, hipStream_t st, const FusedArgs& A) {
-        hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, FAST>), dim3(k1_blocks(P)), dim3(cols::kK1Threads), 0, st,
-                           P, k1_args(A));
+        hipLaunchKernelGGL((cols::k_fused_cols<4, FS, IN, FAST, kColsF32>), dim3(k1_blocks(P)),
+                           dim3(cols::kK1Threads), 0, st, P, k1_args(A));
     }
 };
-
-bool seq_fused_supported(const Params& P) { return fused_cols_supported(P) && P.ring == 0; }
-// Untiled frames, a tiled context's whole frame and its border launch (the
-// ring of K1 blocks + the tile's TAA; the last work-group forwards the reach
-// report).
-bool frame_fused_supported(const Params& P) { return fused_supported(P); }
 
 template <int FS, class IN, bool FAST>
 struct LaunchFrameOne {
     static void go(const Params& P, hipStream_t st, const FusedArgs& A) {
         const int nk1 = P.ring < 0 || P.nbx <= 0 || P.nby <= 0 ? 0 : k1_blocks(P), nk1p = (nk1 + 7) & ~7;
         const int nk2 = frame_taa_tiles<cols::kK1Threads>(P);
-        hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN, true, FAST>), dim3(nk1p + nk2), dim3(cols::kK1Threads),
-                           0, st, P, k1_args(A), P, taa_args(A), nk1, nk1p);
+        hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN, true, FAST, kColsF32>), dim3(nk1p + nk2),
+                           dim3(cols::kK1Threads), 0, st, P, k1_args(A), P, taa_args(A), nk1, nk1p);
     }
 };
-
-hipError_t launch_fused_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
-    if (!fused_cols_supported(P)) return launch_fused_rows_frame_one(P, st, A);  // f32 tmp_data
-    dispatch_cols<LaunchFrameOne>(P, P, st, A);
-    return hipGetLastError();
-}
 
 template <int FS, class IN, bool FAST>
 struct LaunchColsTaa {
@@ -1030,21 +1200,62 @@ struct LaunchColsTaa {
         const int nk2 = A2 ? frame_taa_tiles<cols::kK1Threads>(P2) : 0;
         if (nk1 + nk2 == 0) return;
         const TaaArgs T = A2 ? taa_args(*A2) : TaaArgs{};
-        hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN, false, FAST>), dim3(nk2 ? nk1p + nk2 : nk1),
+        hipLaunchKernelGGL((cols::k_fused_cols_taa<4, FS, IN, false, FAST, kColsF32>), dim3(nk2 ? nk1p + nk2 : nk1),
                            dim3(cols::kK1Threads), 0, st, A ? P : P2, k1_args(A ? *A : *A2), A2 ? P2 : P, T, nk1,
                            nk1p);
     }
 };
 
-hipError_t launch_fused_k1_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
-                               const FusedArgs* A2) {
+}  // namespace
+
+template <>
+hipError_t launch_cols_k1<kColsF32>(const Params& P, hipStream_t st, const FusedArgs& A) {
+    dispatch_cols<LaunchCols>(P, P, st, A);
+    return hipGetLastError();
+}
+template <>
+hipError_t launch_cols_frame_one<kColsF32>(const Params& P, hipStream_t st, const FusedArgs& A) {
+    dispatch_cols<LaunchFrameOne>(P, P, st, A);
+    return hipGetLastError();
+}
+template <>
+hipError_t launch_cols_k1_taa<kColsF32>(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
+                                        const FusedArgs* A2) {
     dispatch_cols<LaunchColsTaa>(A ? P : P2, P, st, A, P2, A2);
     return hipGetLastError();
 }
 
-hipError_t launch_fused_k1_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
-    dispatch_cols<LaunchCols>(P, P, st, A);
-    return hipGetLastError();
+#if !BMFR_COLS_F32
+// f32 tmp_data with fast_fit runs the column-split K1 too
+// (bmfr_fused_cols_f32.hip); -DBMFR_F32_ROWS=1 keeps the row-split K1 of
+// bmfr_fused.hip for it (A/B).
+#ifndef BMFR_F32_ROWS
+#define BMFR_F32_ROWS 0
+#endif
+bool fused_cols_supported(const Params& P) {
+    return (P.half_tmp || (!BMFR_F32_ROWS && (P.fast_fit || BMFR_F32_COLS_EXACT))) && fused_supported(P);
 }
+
+bool seq_fused_supported(const Params& P) { return fused_cols_supported(P) && P.ring == 0; }
+// Untiled frames, a tiled context's whole frame and its border launch (the
+// ring of K1 blocks + the tile's TAA; the last work-group forwards the reach
+// report).
+bool frame_fused_supported(const Params& P) { return fused_supported(P); }
+
+hipError_t launch_fused_frame_one(const Params& P, hipStream_t st, const FusedArgs& A) {
+    if (!fused_cols_supported(P)) return launch_fused_rows_frame_one(P, st, A);  // f32 tmp_data, BMFR_F32_ROWS
+    return P.half_tmp ? launch_cols_frame_one<false>(P, st, A) : launch_cols_frame_one<true>(P, st, A);
+}
+
+hipError_t launch_fused_k1_taa(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
+                               const FusedArgs* A2) {
+    return (A ? P : P2).half_tmp ? launch_cols_k1_taa<false>(P, st, A, P2, A2)
+                                 : launch_cols_k1_taa<true>(P, st, A, P2, A2);
+}
+
+hipError_t launch_fused_k1_cols(const Params& P, hipStream_t st, const FusedArgs& A) {
+    return P.half_tmp ? launch_cols_k1<false>(P, st, A) : launch_cols_k1<true>(P, st, A);
+}
+#endif
 
 }  // namespace bmfr

@@ -153,8 +153,11 @@ __device__ __forceinline__ void k1_block(const Params& P, int g, int& bx, int& b
 
 // Linear index of image pixel (x, y) in a plane of the buffer region, and
 // clamps into the region (= the image when untiled).
+// (y - oy) and the stride are below 2^24 for every valid context (a plane is
+// at most 4 GiB and at least 32 pixels high, validate() in bmfr_capi.hip), so
+// the row offset is one 24-bit multiply-add (v_mad_u32_u24, full rate).
 __device__ __forceinline__ uint32_t pix(const Params& P, int x, int y) {
-    return (uint32_t)((y - P.oy) * P.stride + (x - P.ox));
+    return __umul24((uint32_t)(y - P.oy), (uint32_t)P.stride) + (uint32_t)(x - P.ox);
 }
 __device__ __forceinline__ int clamp_rx(const Params& P, int x) { return min(max(x, P.ox), P.ox + P.stride - 1); }
 __device__ __forceinline__ int clamp_ry(const Params& P, int y) { return min(max(y, P.oy), P.oy + P.rows - 1); }
@@ -408,27 +411,10 @@ __device__ __forceinline__ NoisyTaps<IN> noisy_taps_issue(const Params& P, const
         for (int i = 0; i < 4; ++i) tp.pp[i] = ld3raw<IN>(in.p_prev, sidx[i]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) tp.pn[i] = ld3raw<IN>(in.n_prev, sidx[i]);
-#if defined(BMFR_PROBE_K1_REC16)  // timing probe (wrong results): 16-byte records {colour, spp}
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint4 q = *reinterpret_cast<const uint4*>(at_byte(in.noisy_prev, sidx[i] * 16u));
-            tp.pc[i] = f3{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z)};
-            tp.spu[i] = q.w & 255u;
-        }
-#elif defined(BMFR_PROBE_K1_REC)  // timing probe (wrong results): colour + spp as one 16-byte load, no spp load
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t lim = (uint32_t)(P.stride * P.rows) * 12u - 16u;  // never past the plane's end
-            const uint4 q = *reinterpret_cast<const uint4*>(at_byte(in.noisy_prev, min(sidx[i] * 12u, lim)));
-            tp.pc[i] = f3{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z)};
-            tp.spu[i] = q.w & 255u;
-        }
-#else
 #pragma unroll
         for (int i = 0; i < 4; ++i) tp.pc[i] = ld3(in.noisy_prev, sidx[i]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) tp.spu[i] = ld_px(in.spp_prev, sidx[i]);
-#endif
         if (FILT) {  // same taps (bmfr.cl:801-832)
 #pragma unroll
             for (int i = 0; i < 4; ++i) tp.pa[i] = ld3(acc_prev, sidx[i]);
