@@ -593,7 +593,7 @@ def main():
         k1_roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": round(achieved / HBM_PEAK_GBS, 4),
                    "traffic": pmc_traffic(workload) if world == 1 else None,
-                   "kernel": "k_fused_cols (K1)" if a.half_tmp else "k_fused (K1)",
+                   "kernel": "k_fused_cols (K1)" if a.half_tmp or a.fast_fit else "k_fused (K1)",
                    "algorithmic_bytes_per_launch": k1_bytes_per_px(s) * tile_px}
         if world == 1:
             k1_roof.update(valu_roofline(a.fast_fit))
@@ -687,7 +687,7 @@ def main():
                  ("_f16in" if b.input_half else "") + ("_fastfit" if b.fast_fit else "")
             line[f"ms_per_frame_{key}"] = variant_line(rv, vs, W, H, wl, "k_fused_cols_taa<..., SAME = true>"
                                                        if b.half_tmp else "k_fused_rows_taa<...>",
-                                                       "k_fused_cols" if b.half_tmp else "k_fused")
+                                                       "k_fused_cols" if b.half_tmp or b.fast_fit else "k_fused")
         if world == 1 and a.cpu_frames > 0:
             line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_frames, a.seed)
         print(json.dumps(line), flush=True)

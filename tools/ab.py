@@ -68,12 +68,19 @@ def time_one(W, H, frames=45, first=5):
     import torch
 
     import bmfr_amd
-    # AB_FAST_FIT=1: time the fast_fit configuration; AB_F32TMP=1: f32 tmp_data
+    # AB_FAST_FIT=1: time the fast_fit configuration; AB_F32TMP=1: f32 tmp_data;
+    # AB_CFG5=1: BASELINE config 5 (third-order features, half input planes)
+    cfg5 = os.environ.get("AB_CFG5") == "1"
     den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H,
                                                 fast_fit=int(os.environ.get("AB_FAST_FIT", "0")),
                                                 use_half_precision_in_tmp_data=0 if os.environ.get("AB_F32TMP") == "1"
-                                                else 1))
+                                                else 1,
+                                                scaled=bmfr_amd.SCALED_THIRD_ORDER if cfg5 else bmfr_amd.SCALED_DEFAULT,
+                                                input_half=int(cfg5)))
     fr = [bmfr_amd.synth_frame_device(W, H, f) for f in range(frames)]
+    if cfg5:
+        fr = [{k: (v.half() if k in ("noisy", "normals", "positions", "albedo") else v) for k, v in x.items()}
+              for x in fr]
     den.set_profiling(True, capacity=frames, stride=1)
     for f in range(frames):
         vp, _ = bmfr_amd.synth_camera(W, H, max(f - 1, 0))

@@ -9,6 +9,14 @@
 //    infinities, quiet NaNs, denormals) and random floats: K2's strip resolve
 //    regroups the min / max of a neighbourhood (min(+0, -0) == min(-0, +0);
 //    only two NaNs of different sign give an order-dependent payload).
+// 3. v_fma_mixlo_f16 / v_fma_mixhi_f16 (f16 result) against v_fma_mix_f32
+//    then v_cvt_pk_f16_f32 on random half / float operands.  Measured: they
+//    differ in 616 of 2^27 halves (the mix instructions do not round through
+//    f32): not for the exact fit, which must round to f32 and then to half as
+//    upstream's float arithmetic + vstore_half; fast_fit's column updates with
+//    them (v_fma_mix{lo,hi}_f16 in place of two v_fma_mix_f32 + v_cvt_pk)
+//    measured K1 +1.8 % (4K fast_fit) and +2.6 % (config 5): the in-place
+//    halves chain each pair's two writes.  Not kept.
 //
 //   hipcc --offload-arch=gfx950 -O3 tools/rcp_check.hip -o tools/rcp_check && ./tools/rcp_check
 #include <hip/hip_runtime.h>
@@ -49,6 +57,31 @@ __global__ void k_comm(const float* v, int n, unsigned long long* bad, uint32_t*
                 pairs[(m * 4 + k) * 2 + 1] = __float_as_uint(b);
             }
         }
+    }
+}
+
+__global__ void k_mix(uint32_t seed, int n, unsigned long long* bad, uint32_t* ex) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t x = seed ^ (uint32_t)i * 2654435761u;
+    auto next = [&]() { x ^= x << 13; x ^= x >> 17; x ^= x << 5; return x; };
+    const uint32_t hb = next(), cb = next();
+    uint32_t fb = next();
+    if ((fb & 3) == 0) fb &= 0x8fffffffu;  // some small multipliers (products near half denormals)
+    const float f = __uint_as_float(fb);
+    float lo, hi;
+    asm volatile("v_fma_mix_f32 %0, -%1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(lo) : "v"(hb), "v"(f), "v"(cb));
+    asm volatile("v_fma_mix_f32 %0, -%1, %2, %3 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(hi) : "v"(hb), "v"(f), "v"(cb));
+    uint32_t ref;
+    asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(ref) : "v"(lo), "v"(hi));
+    uint32_t got = cb;
+    asm volatile("v_fma_mixlo_f16 %0, -%1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(got) : "v"(hb), "v"(f));
+    asm volatile("v_fma_mixhi_f16 %0, -%1, %2, %0 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "+v"(got) : "v"(hb), "v"(f));
+    // NaN results: any NaN bit pattern counts as equal
+    const bool nl = (ref & 0x7c00u) == 0x7c00u && (ref & 0x3ffu), nh = (ref & 0x7c000000u) == 0x7c000000u && (ref & 0x3ff0000u);
+    const uint32_t m = (nl ? 0u : 0xffffu) | (nh ? 0u : 0xffff0000u);
+    if ((ref & m) != (got & m)) {
+        if (atomicAdd(bad, 1ull) == 0) { ex[0] = hb; ex[1] = fb; ex[2] = cb; ex[3] = ref; ex[4] = got; }
     }
 }
 
@@ -94,5 +127,16 @@ int main() {
     // survives) depend on the order; +0 / -0, infinities and NaN / number
     // pairs do not.  K2's regrouped min / max never see a NaN (tone-mapped
     // YCoCg values are finite).
-    return h[0] + h[1] > 4 ? 1 : 0;
+    const unsigned long long rcp_bad = h[0], cmp_bad = h[1];
+    uint32_t* dx;
+    (void)hipMalloc(&dx, 5 * 4);
+    (void)hipMemset(bad, 0, 16);
+    const int nm = 1 << 26;
+    hipLaunchKernelGGL(k_mix, dim3(nm / 256), dim3(256), 0, 0, 0x9e3779b9u, nm, bad, dx);
+    uint32_t xm[5] = {};
+    (void)hipMemcpy(h, bad, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(xm, dx, sizeof xm, hipMemcpyDeviceToHost);
+    std::printf("v_fma_mixlo/hi_f16 vs cvt_pk(v_fma_mix_f32): %llu mismatches over %d operand triples\n", h[0], nm);
+    if (h[0]) std::printf("  h 0x%08x f 0x%08x c 0x%08x: cvt 0x%08x mix 0x%08x\n", xm[0], xm[1], xm[2], xm[3], xm[4]);
+    return rcp_bad + cmp_bad > 4 ? 1 : 0;
 }
