@@ -193,14 +193,30 @@ def cpu_baseline(cfg: bmfr_amd.BmfrConfig, frames: int, seed: int):
 
 
 def pmc_traffic(workload: str):
-    """HBM bytes per K1 launch from the committed rocprofv3 PMC summary
-    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), when one exists for this workload."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), when one exists for this
+    workload: `<workload>` K1, `<workload>_k2` K2, `<workload>_frame` the
+    one-launch frame kernel, `<workload>_two_launch` K1 + K2 of one frame."""
     p = os.path.join(ROOT, "profiles", "pmc_k1.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
         d = json.load(f)
     return d.get(workload, {}).get("hbm_bytes_per_launch")
+
+
+def with_traffic(roof: dict, workload_key: str, launch_ms: float) -> dict:
+    """roof plus the launch's measured HBM bytes (pmc_traffic) as a rate:
+    the algorithmic roofline counts compulsory bytes only, while K2 also
+    re-reads K1's intermediates (accumulated colour, reprojected positions:
+    20 B/px) -- its bound is the bytes it actually moves."""
+    t = pmc_traffic(workload_key)
+    roof["traffic"] = t
+    if t and launch_ms:
+        g = t / (launch_ms * 1e-3) / 1e9
+        roof["traffic_gbs"] = round(g, 1)
+        roof["traffic_frac"] = round(g / HBM_PEAK_GBS, 4)
+    return roof
 
 
 PROF_STRIDE = 10  # timed frames between two recorded with per-kernel events
@@ -456,9 +472,11 @@ def variant_line(r, s: int, W: int, H: int, workload: str, kernel: str, k1_kerne
         kb = k1_bytes_per_px(s) * W * H
         ka = kb / (r["k1_ms"] * 1e-3) / 1e9
         return dict(side_line(r), workload=workload,
-                    roofline={"bound": "hbm", "achieved": round(ka, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": round(ka / HBM_PEAK_GBS, 4), "kernel": k1_kernel + " (K1; frame = K1, K2)",
-                              "algorithmic_bytes_per_launch": kb, "launch_ms": round(r["k1_ms"], 4)})
+                    roofline=with_traffic({"bound": "hbm", "achieved": round(ka, 1), "peak": HBM_PEAK_GBS,
+                                           "unit": "GB/s", "frac": round(ka / HBM_PEAK_GBS, 4),
+                                           "kernel": k1_kernel + " (K1; frame = K1, K2)",
+                                           "algorithmic_bytes_per_launch": kb, "launch_ms": round(r["k1_ms"], 4)},
+                                          workload, r["k1_ms"]))
     fb = frame_bytes_per_px(s) * W * H
     fa = fb / (r["frame_kernel_ms"] * 1e-3) / 1e9
     return dict(side_line(r), workload=workload,
@@ -591,10 +609,11 @@ def main():
     if rank == 0:
         achieved = k1_bytes_per_px(s) * tile_px / (r["k1_ms"] * 1e-3) / 1e9
         k1_roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": round(achieved / HBM_PEAK_GBS, 4),
-                   "traffic": pmc_traffic(workload) if world == 1 else None,
+                   "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                    "kernel": "k_fused_cols (K1)" if a.half_tmp or a.fast_fit else "k_fused (K1)",
                    "algorithmic_bytes_per_launch": k1_bytes_per_px(s) * tile_px}
+        if world == 1:
+            with_traffic(k1_roof, workload, r["k1_ms"])
         if world == 1:
             k1_roof.update(valu_roofline(a.fast_fit))
         # Untiled per-frame runs below kTwoLaunchBlocks K1 blocks (bmfr_sizes
@@ -661,9 +680,10 @@ def main():
         if world == 1:
             k2 = k2_bytes_per_px(s) * tile_px / (r["k2_ms"] * 1e-3) / 1e9 if not a.sequence else None
             if k2:
-                line["roofline_k2"] = {"bound": "hbm", "achieved": round(k2, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                       "frac": round(k2 / HBM_PEAK_GBS, 4), "kernel": "k_fused_taa (K2)",
-                                       "algorithmic_bytes_per_launch": k2_bytes_per_px(s) * tile_px}
+                line["roofline_k2"] = with_traffic(
+                    {"bound": "hbm", "achieved": round(k2, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(k2 / HBM_PEAK_GBS, 4), "kernel": "k_fused_taa (K2)",
+                     "algorithmic_bytes_per_launch": k2_bytes_per_px(s) * tile_px}, workload + "_k2", r["k2_ms"])
         if rseq is not None:
             line["ms_per_frame_sequence"] = side_line(rseq)
         if r1080 is not None:

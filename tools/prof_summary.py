@@ -6,6 +6,10 @@
   prof_summary.py calib <dir> <counter> <bytes>   counter / true bytes per calibration kernel
   prof_summary.py traffic <fetch_dir> <write_dir> <workload> <pixels> <alg_bytes_per_px>
                                        -> profiles/pmc_k1.json entry (HBM bytes per K1 launch)
+  prof_summary.py traffic2 <fetch_dir> <write_dir> <workload> <pixels> <k1_alg_per_px> <k2_alg_per_px>
+                                       -> pmc_k1.json entries <workload> (K1), <workload>_k2 (K2)
+                                          and <workload>_two_launch (K1 + K2 of a frame), from
+                                          the separate-launch passes (tools/k1_frames.py)
   prof_summary.py sq <out.json> <dir> [<dir> ...] -> K1 / K2 per-launch means of every counter
                                        in the passes, plus derived rates
 
@@ -133,25 +137,32 @@ def main():
         d = sq(sys.argv[3:])
         json.dump(d, open(path, "w"), indent=1)
         print(json.dumps(d, indent=1))
-    elif cmd == "traffic":
+    elif cmd in ("traffic", "traffic2"):
         fetch_dir, write_dir, workload, px, alg = sys.argv[2:7]
-        k1 = os.environ.get("K1_NAME", "k_fused_cols<4, 6")
+        fetch, write = pmc(fetch_dir, "FETCH_SIZE"), pmc(write_dir, "WRITE_SIZE")
 
-        def pick(d):
-            return next(v for k, v in d.items() if k.startswith(k1))
-        f = pick(pmc(fetch_dir, "FETCH_SIZE"))
-        w = pick(pmc(write_dir, "WRITE_SIZE"))
-        entry = {"fetch_kb_raw": f, "write_kb": w,
-                 "hbm_bytes_per_launch": (2 * f + w) * 1024,
-                 "hbm_bytes_per_launch_raw": (f + w) * 1024,
-                 "algorithmic_bytes_per_launch": int(px) * int(alg),
-                 "note": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE half-count correction, "
-                         "MI355X_MICROARCH.md HBM); raw = FETCH_SIZE + WRITE_SIZE"}
+        def entry(name, alg_bytes):
+            f = next(v for k, v in fetch.items() if k.startswith(name))
+            w = next(v for k, v in write.items() if k.startswith(name))
+            return {"fetch_kb_raw": f, "write_kb": w,
+                    "hbm_bytes_per_launch": (2 * f + w) * 1024,
+                    "hbm_bytes_per_launch_raw": (f + w) * 1024,
+                    "algorithmic_bytes_per_launch": alg_bytes,
+                    "note": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE half-count correction, "
+                            "MI355X_MICROARCH.md HBM); raw = FETCH_SIZE + WRITE_SIZE"}
         path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_k1.json")
         d = json.load(open(path)) if os.path.exists(path) else {}
-        d[workload] = entry
+        new = {workload: entry(os.environ.get("K1_NAME", "k_fused_cols<4, 6"), int(px) * int(alg))}
+        if cmd == "traffic2":
+            k1, k2 = new[workload], entry(os.environ.get("K2_NAME", "k_fused_taa<float>"), int(px) * int(sys.argv[7]))
+            new[workload + "_k2"] = k2
+            new[workload + "_two_launch"] = {
+                k: k1[k] + k2[k] for k in ("fetch_kb_raw", "write_kb", "hbm_bytes_per_launch",
+                                           "hbm_bytes_per_launch_raw", "algorithmic_bytes_per_launch")}
+            new[workload + "_two_launch"]["note"] = "K1 + K2 launches of one frame (the 4K frames' form); " + k1["note"]
+        d.update(new)
         json.dump(d, open(path, "w"), indent=1)
-        print(json.dumps(entry, indent=1))
+        print(json.dumps(new, indent=1))
 
 
 if __name__ == "__main__":
