@@ -5,6 +5,7 @@ production schedule, one launch each, unlike libbmfr's per-kernel
 profiling, which splits K1 and K2), averaged over runs of 10 frames.
 
   python tools/frame_times.py [W H FRAMES [PASSES]] [--third-order] [--input-half] [--f32-tmp]
+  (FRAME_LAUNCHES=1 or 2 forces one launch per frame or K1, K2)
 """
 import os
 import sys
@@ -24,6 +25,9 @@ frames = [a.render(f) for f in range(N)]
 # All passes enqueued back to back (contexts made up front, one synchronize at
 # the end): the GPU never idles between passes.
 dens = [bmfr_amd.Denoiser(cfg) for _ in range(P)]
+if os.environ.get("FRAME_LAUNCHES"):  # 1 / 2: force the frame's launch form (bmfr_debug_frame_launches)
+    for d in dens:
+        d.debug_frame_launches(int(os.environ["FRAME_LAUNCHES"]))
 evs = [[torch.cuda.Event(enable_timing=True) for _ in range(N + 1)] for _ in range(P)]
 torch.cuda.synchronize()
 for rep in range(P):
