@@ -271,22 +271,28 @@ __device__ __forceinline__ void update_column(h2 (&a)[8], const float (&u)[kSlot
 // (bmfr.cl:608-617: tmp * u_vec, then +=) -- chains (0, 1) and (2, 3) as
 // packed pairs, every lane rounding as the scalar ops --, reduced in
 // upstream's association; then the update of bmfr.cl:646 as in
-// update_column (packed Markstein quotients, rows above the pivot kept) or,
-// with FAST (fast_fit: the fused update only, as the row-split f32 K1), one
-// fused multiply-add per element on RN(c2 / |u|^2).
-template <int c>
+// update_column (packed Markstein quotients, rows above the pivot kept).
+// FAST (fast_fit): fused dot chains, the butterfly sum, and one fused
+// multiply-add per element on RN(c2 / |u|^2).
+template <int c, bool FAST>
 __device__ __forceinline__ void update_column_f32(f2v (&a)[8], const float (&u)[kSlots], float ulen2, float recip,
-                                                  int l, bool fast) {
+                                                  int l) {
     f2v p01 = {0.f, 0.f}, p23 = {0.f, 0.f};
 #pragma unroll
     for (int si = 0; si < 4; ++si) {
-        p01 = p01 + a[2 * si] * f2v{u[4 * si], u[4 * si + 1]};
-        p23 = p23 + a[2 * si + 1] * f2v{u[4 * si + 2], u[4 * si + 3]};
+        const f2v u01 = {u[4 * si], u[4 * si + 1]}, u23 = {u[4 * si + 2], u[4 * si + 3]};
+        if constexpr (FAST) {  // fused
+            p01 = __builtin_elementwise_fma(a[2 * si], u01, p01);
+            p23 = __builtin_elementwise_fma(a[2 * si + 1], u23, p23);
+        } else {
+            p01 = p01 + a[2 * si] * u01;
+            p23 = p23 + a[2 * si + 1] * u23;
+        }
         if (si == 0) p01.x = l >= c ? p01.x : 0.f;  // rows above the pivot: skipped
     }
     const float p[4] = {p01.x, p01.y, p23.x, p23.y};
-    const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);
-    if (fast) {  // wave-uniform
+    const float c2 = 2.f * wave_reduce<RedOp::Sum, FAST>(p);
+    if constexpr (FAST) {
         const float sc = c2 * recip;
         const f2v vs = {sc, sc};
         const float keep0 = a[0].x;
@@ -424,13 +430,14 @@ __device__ __forceinline__ void wait_all_progress(LDS& L, int c) {
 
 // The owner of pivot column c (>= 1), once steps 0..c-1 are applied to it:
 // |x|^2 over rows >= c+1, the Householder vector u and |u|^2 (bmfr.cl:555-601),
-// published to LDS with the R column.  FAST (half tmp_data only): hardware
-// sqrt / reciprocal, butterfly sum, u published as the column's halves.
+// published to LDS with the R column.  FAST (fast_fit): hardware sqrt /
+// reciprocal, butterfly sum, fused squares; with half tmp_data u published
+// as the column's halves (HALVES), with f32 tmp_data as floats.
 template <int c, int B, int NW, bool FAST = false, class P2, class LDS>
 __device__ __forceinline__ void publish_pivot(const P2 (&a)[8], LDS& L, int l) {
     constexpr int RE = B - 2;
     constexpr bool F32 = std::is_same_v<P2, f2v>;
-    static_assert(!(FAST && F32), "f32 tmp_data publishes f32 pivots");
+    constexpr bool HALVES = FAST && !F32;
     float x[kSlots];
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) x[j] = hget(a, j);
@@ -445,7 +452,7 @@ __device__ __forceinline__ void publish_pivot(const P2 (&a)[8], LDS& L, int l) {
         for (int si = 0; si < 4; ++si) {
             const int j = m + 4 * si;
             const float xj = j == 0 && l < c + 1 ? 0.f : x[j];
-            if constexpr (F32) s = s + xj * xj;
+            if constexpr (F32 && !FAST) s = s + xj * xj;
             else s = __builtin_fmaf(xj, xj, s);
         }
         p[m] = s;
@@ -460,7 +467,7 @@ __device__ __forceinline__ void publish_pivot(const P2 (&a)[8], LDS& L, int l) {
     if (l == c) x[0] = ucl2;
     constexpr int buf = c % kUBufs;
     if constexpr (c >= kUBufs) wait_all_progress<NW>(L, c - kUBufs);  // readers of u_{c-3} done
-    if constexpr (FAST) {  // u as the column's halves, rows <= c zeroed; the pivot element in piv[2]
+    if constexpr (HALVES) {  // u as the column's halves, rows <= c zeroed; the pivot element in piv[2]
         uint32_t w[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) w[k] = __builtin_bit_cast(uint32_t, a[k]);
@@ -502,9 +509,10 @@ __device__ __forceinline__ void k1_barrier() { lds_barrier(); }
 template <int NS, int FS, int NW = 4, bool FAST = false, bool F32 = false>
 struct WaveFit {
     static constexpr int B = NS + FS + 3;
-    // fast_fit: the fused trailing update (FAST); with half tmp_data also the
-    // butterfly reductions, f32 noise add and hardware sqrt / reciprocals
-    // (FASTR) -- f32 tmp_data fuses the update only, as the row-split K1 did.
+    // fast_fit (FAST): the fused trailing update, butterfly reductions, f32
+    // noise add, hardware sqrt / reciprocals, scaling by the reciprocal; with
+    // half tmp_data (FASTR) also u published as halves (the update on v_dot2 /
+    // v_fma_mix).
     static constexpr bool FASTR = FAST && !F32;
     using P2 = Pair<F32>;
     static constexpr int NF = B - 3;  // pivot columns
@@ -532,14 +540,14 @@ struct WaveFit {
         const bool publish = nxt < NF && W == owner(nxt);
         if constexpr (c == 0) {
             if (publish) {  // column 1 of wave 0: its first column
-                update_column0<FASTR>(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre[0], NP > 0, noise2);
-                publish_pivot<nxt, B, NW, FASTR>(a[slot(nxt)], L, l);
+                update_column0<FAST>(a[slot(nxt)], l, noise + (nxt - 1) * kBlockPixels, pre[0], NP > 0, noise2);
+                publish_pivot<nxt, B, NW, FAST>(a[slot(nxt)], L, l);
             }
             sfor<NSL>([&](auto K) {
                 constexpr int k = decltype(K)::value;
                 const int fb = 1 + W + NW * k;
                 if (owns(W, fb) && !(publish && fb == nxt))  // slots < NP: feature columns, prefetched
-                    update_column0<FASTR>(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr,
+                    update_column0<FAST>(a[k], l, fb < NF ? noise + (fb - 1) * kBlockPixels : nullptr,
                                    pre[k < kPre ? k : 0], k < NP, noise2);
             });
         } else {
@@ -568,14 +576,14 @@ struct WaveFit {
                 }
                 const float ulen2 = L.piv[c % kUBufs][0], recip = L.piv[c % kUBufs][1];
                 auto upd = [&](P2 (&col)[8]) {
-                    if constexpr (F32) update_column_f32<c>(col, u, ulen2, recip, l, FAST);
+                    if constexpr (F32) update_column_f32<c, FAST>(col, u, ulen2, recip, l);
                     else if constexpr (FAST) update_column_fast<c>(col, uh, uc, recip);
                     else update_column<c>(col, u, ulen2, recip, l);
                 };
                 if constexpr (nxt < NF) {
                     if (publish) {  // the next pivot is every wave's critical path: issue it first
                         upd(a[slot(nxt)]);
-                        publish_pivot<nxt, B, NW, FASTR>(a[slot(nxt)], L, l);
+                        publish_pivot<nxt, B, NW, FAST>(a[slot(nxt)], L, l);
                     }
                 }
                 sfor<NSL>([&](auto K) {
@@ -676,8 +684,8 @@ struct WaveFit {
                         lo[m] = fminf(v, lo[m]);
                     }
                 }
-                const float bmax = wave_reduce<RedOp::Max, FASTR>(hi);
-                const float bmin = wave_reduce<RedOp::Min, FASTR>(lo);
+                const float bmax = wave_reduce<RedOp::Max, FAST>(hi);
+                const float bmin = wave_reduce<RedOp::Min, FAST>(lo);
                 const float d = bmax - bmin;
                 const bool divide = fabsf(d) > 1.0f;  // scale(), bmfr.cl:200-205
                 const float rcp = 1.f / d;
@@ -690,7 +698,7 @@ struct WaveFit {
                 for (int j = 0; j < kSlots; ++j) {
                     const float v = hget(a[k], j) - bmin;
                     // fast_fit: one multiply by the rounded reciprocal (as phase 3)
-                    const float sv = FASTR ? v * rcp : div_by_recip(v, d, rcp);
+                    const float sv = FAST ? v * rcp : div_by_recip(v, d, rcp);
                     hset(a[k], j, divide ? sv : v);
                 }
             }
@@ -1005,7 +1013,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
                 f2v v = {feature_value(f, nrm[2 * h], wp[2 * h]), feature_value(f, nrm[2 * h + 1], wp[2 * h + 1])};
                 if (f >= NS) {
                     v = v - f2v{bmin, bmin};
-                    if (FASTR) {
+                    if (FAST) {
                         if (fabsf(d) > 1.0f) v = v * f2v{rcp, rcp};  // fast_fit: as the fit scaled it
                     } else if (fabsf(d) > 1.0f) {
                         const f2v q0 = v * f2v{rcp, rcp};
