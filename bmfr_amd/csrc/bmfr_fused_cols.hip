@@ -68,9 +68,23 @@ constexpr int m_slots() { return F32 ? kSlots - 4 : kSlots; }
 constexpr bool keep_in_m(int B, bool F32 = false) {
     return (B - 1) * 64 * (F32 ? 4 * m_slots<true>() : 2 * kSlots) >= (kUBufs * 64 * kUStride + kKeep) * 4;
 }
+// What the fit writes for back substitution and phase 3: R[x][y][ch] (x =
+// column, as k_fused), the weights, per scaled feature min, max,
+// 1/(max-min).  Written only once the fit has loaded its columns.
+template <int B>
+struct FitOut {
+    float R[(B - 2) * (B - 2) * 3];
+    float weights[(B - 3) * 3];
+    float mm[3 * (B - 3)];
+};
 template <int B, int NW = 4, bool F32 = false>
 struct Lds {
     using MT = std::conditional_t<F32, float, _Float16>;
+    static constexpr int kMBytes = (B - 1) * 64 * m_slots<F32>() * (F32 ? 4 : 2);
+    static constexpr int kUKBytes = (kUBufs * 64 * kUStride + (keep_in_m(B, F32) ? kKeep : 1)) * 4;
+    // FitOut in the matrix area's tail, beside the u buffers (and the kept
+    // colours), where it has room
+    static constexpr bool kTail = kMBytes - kUKBytes >= (int)sizeof(FitOut<B>);
     union {
         // design matrix after phase 1, column c at M[c - 1], [lane * 16 + j]
         // (half pairs swizzled by lane, see run()); F32: [lane * 12 + 4 q' + j % 4],
@@ -79,8 +93,14 @@ struct Lds {
         struct {
             float u[kUBufs][64 * kUStride];  // Householder vectors, u_c in buffer c % kUBufs
             float keep_m[keep_in_m(B, F32) ? kKeep : 1];
+            FitOut<B> fo_tail[kTail ? 1 : 0];
         };
     };
+    FitOut<B> fo_own[kTail ? 0 : 1];
+    __device__ FitOut<B>& fo() {
+        if constexpr (kTail) return fo_tail[0];
+        else return fo_own[0];
+    }
     float keep_s[keep_in_m(B, F32) ? 1 : kKeep];
     __device__ float* keep() { return keep_in_m(B, F32) ? keep_m : keep_s; }  // [(item * 3 + ch) * 64 NW + t]
     float piv[kUBufs][3];               // |u|^2 and RN(1/|u|^2) of the published vector; fast_fit: u's pivot element
@@ -90,9 +110,6 @@ struct Lds {
     int max_polls;                      // Params::max_polls (kept here: read only once a flag is not ready)
     int delay;                          // Params::debug_delay (diagnostics, read at the block's end)
     int flag;                           // one-launch frame: index of this block's completion flag
-    float R[(B - 2) * (B - 2) * 3];     // R[x][y][ch], x = column (as k_fused)
-    float weights[(B - 3) * 3];
-    float mm[3 * (B - 3)];              // per scaled feature: min, max, 1/(max-min)
 };
 static_assert(sizeof(float) * kUBufs * 64 * kUStride <= sizeof(_Float16) * 12 * 64 * kSlots,
               "u buffers must fit in the matrix area (B >= 13)");
@@ -487,11 +504,11 @@ __device__ __forceinline__ void publish_pivot(const P2 (&a)[8], LDS& L, int l) {
     }
     if (l < c) {  // R column: rows above the diagonal, then the diagonal
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) L.R[(c * RE + l) * 3 + ch] = x[0];
+        for (int ch = 0; ch < 3; ++ch) L.fo().R[(c * RE + l) * 3 + ch] = x[0];
     }
     if (l == c) {
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) L.R[(c * RE + c) * 3 + ch] = vlen;
+        for (int ch = 0; ch < 3; ++ch) L.fo().R[(c * RE + c) * 3 + ch] = vlen;
     }
     // u_c and |u_c|^2 in LDS before the flag says so
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
@@ -690,9 +707,9 @@ struct WaveFit {
                 const bool divide = fabsf(d) > 1.0f;  // scale(), bmfr.cl:200-205
                 const float rcp = 1.f / d;
                 if (l == 0) {
-                    L.mm[3 * (c - NS)] = bmin;
-                    L.mm[3 * (c - NS) + 1] = bmax;
-                    L.mm[3 * (c - NS) + 2] = rcp;
+                    L.fo().mm[3 * (c - NS)] = bmin;
+                    L.fo().mm[3 * (c - NS) + 1] = bmax;
+                    L.fo().mm[3 * (c - NS) + 2] = rcp;
                 }
 #pragma unroll
                 for (int j = 0; j < kSlots; ++j) {
@@ -703,7 +720,7 @@ struct WaveFit {
                 }
             }
         });
-        if (W == 0 && l < 3) L.R[l] = 32.f;  // R(0,0) = |column 0|
+        if (W == 0 && l < 3) L.fo().R[l] = 32.f;  // R(0,0) = |column 0|
 
 #ifndef BMFR_PROBE_K1_NOQR  // timing probe (wrong results): no Householder steps
         steps(a, L, W, l, noise, pre, noise2, std::make_integer_sequence<int, NF>{});
@@ -714,7 +731,7 @@ struct WaveFit {
             constexpr int k = decltype(K)::value;
             const int c = 1 + W + NW * k;
             if (owns(W, c) && c >= NF) {
-                if (l < NF) L.R[((B - 3) * (B - 2) + l) * 3 + (c - NF)] = hget(a[k], 0);
+                if (l < NF) L.fo().R[((B - 3) * (B - 2) + l) * 3 + (c - NF)] = hget(a[k], 0);
             }
         });
     }
@@ -747,7 +764,7 @@ __device__ __forceinline__ void back_substitute_regs(LDS& L, int t) {
     const bool live = ch < 3 && x < RE;
     float col[RE - 1];  // rows 0..RE-2 of column x
 #pragma unroll
-    for (int y = 0; y < RE - 1; ++y) col[y] = live ? L.R[(x * RE + y) * 3 + ch] : 0.f;
+    for (int y = 0; y < RE - 1; ++y) col[y] = live ? L.fo().R[(x * RE + y) * 3 + ch] : 0.f;
     sfor<RE - 1>([&](auto I) {
         constexpr int i = RE - 2 - decltype(I)::value;
         const float div = row_bcast<i>(col[i]);
@@ -774,7 +791,7 @@ __device__ __forceinline__ void back_substitute_regs(LDS& L, int t) {
     });
     if (ch < 3 && x == RE - 1) {
 #pragma unroll
-        for (int y = 0; y < B - 3; ++y) L.weights[y * 3 + ch] = col[y];
+        for (int y = 0; y < B - 3; ++y) L.fo().weights[y * 3 + ch] = col[y];
     }
 }
 
@@ -999,14 +1016,14 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     for (int hh = 0; hh < NH; ++hh) {
 #pragma unroll
         for (int f = 0; f < B - 3; ++f) {
-            const f2v wv[3] = {f2v{L.weights[3 * f], L.weights[3 * f]},
-                               f2v{L.weights[3 * f + 1], L.weights[3 * f + 1]},
-                               f2v{L.weights[3 * f + 2], L.weights[3 * f + 2]}};
+            const f2v wv[3] = {f2v{L.fo().weights[3 * f], L.fo().weights[3 * f]},
+                               f2v{L.fo().weights[3 * f + 1], L.fo().weights[3 * f + 1]},
+                               f2v{L.fo().weights[3 * f + 2], L.fo().weights[3 * f + 2]}};
             float bmin = 0.f, d = 0.f, rcp = 0.f;
             if (f >= NS) {
-                bmin = L.mm[3 * (f - NS)];
-                d = L.mm[3 * (f - NS) + 1] - bmin;
-                rcp = L.mm[3 * (f - NS) + 2];
+                bmin = L.fo().mm[3 * (f - NS)];
+                d = L.fo().mm[3 * (f - NS) + 1] - bmin;
+                rcp = L.fo().mm[3 * (f - NS) + 2];
             }
 #pragma unroll
             for (int h = kPairs ? hh : 0; h < (kPairs ? hh + 1 : NPR); ++h) {
@@ -1097,9 +1114,15 @@ constexpr int kMinWavesSimd = BMFR_K1_MIN_WAVES;
 #else
 constexpr int kMinWavesSimd = kNW == 4 ? 4 : 6;
 #endif
+// Config 5 (B = 16, fast_fit): -DBMFR_K1_WAVES9F=5 asks for five work-groups
+// per CU (its LDS allows them since FitOut sits in the matrix area's tail).
+#ifndef BMFR_K1_WAVES9F
+#define BMFR_K1_WAVES9F kMinWavesSimd
+#endif
 template <int FS, bool F32, bool FAST>
 constexpr int min_waves() {
-    return F32 ? (FS == 6 ? (FAST ? BMFR_F32_WAVES6 : BMFR_F32_WAVES6X) : BMFR_F32_WAVES9) : kMinWavesSimd;
+    return F32 ? (FS == 6 ? (FAST ? BMFR_F32_WAVES6 : BMFR_F32_WAVES6X) : BMFR_F32_WAVES9)
+               : (FS == 9 && FAST ? BMFR_K1_WAVES9F : kMinWavesSimd);
 }
 
 // FAST: bmfr_config.fast_fit (the fused trailing update, update_column).
