@@ -103,7 +103,7 @@ struct Lds {
     }
     float keep_s[keep_in_m(B, F32) ? 1 : kKeep];
     __device__ float* keep() { return keep_in_m(B, F32) ? keep_m : keep_s; }  // [(item * 3 + ch) * 64 NW + t]
-    float piv[kUBufs][3];               // |u|^2 and RN(1/|u|^2) of the published vector; fast_fit: u's pivot element
+    float piv[kUBufs][3];               // |u|^2 and RN(1/|u|^2) (fast_fit: 2 RN(1/|u|^2)) of the published vector; fast_fit: u's pivot element
     int pub;                            // highest published pivot column
     int prog[NW];                       // per wave: the last step it has applied
     int timeout;                        // a flag wait of this block gave up (reported once, at the end)
@@ -210,13 +210,14 @@ __device__ __forceinline__ float fma_h(h2 h, float b, float s) {
 #define BMFR_FAST_SCHED_BARRIER 1
 #endif
 template <int c>
-__device__ __forceinline__ void update_column_fast(h2 (&a)[8], const h2 (&uh)[8], float uc, float recip) {
-    float p[4];
+__device__ __forceinline__ void update_column_fast(h2 (&a)[8], const h2 (&uh)[8], float uc, float recip2) {
+    // one chain per lane: the pivot row's product (lane c) first -- its
+    // mixed FMA on 0 starts the chain, no zeroed accumulators -- then the
+    // eight v_dot2 pairs
+    float s = fma_h<0>(a[0], uc, 0.f);
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-        p[m] = __builtin_amdgcn_fdot2(a[m + 4], uh[m + 4], __builtin_amdgcn_fdot2(a[m], uh[m], 0.f, false), false);
-    p[0] = fma_h<0>(a[0], uc, p[0]);  // the pivot row (lane c)
-    const float sc = 2.f * wave_reduce_fast<RedOp::Sum>(p) * recip;
+    for (int k = 0; k < 8; ++k) s = __builtin_amdgcn_fdot2(a[k], uh[k], s, false);
+    const float sc = wave_reduce_fast<RedOp::Sum>(s) * recip2;  // = RN(RN(2 dot) RN(1/|u|^2)): doubling is exact
 #pragma unroll
     for (int k = 0; k < kSlots / 2; ++k) {
         float lo, hi;
@@ -308,9 +309,8 @@ __device__ __forceinline__ void update_column_f32(f2v (&a)[8], const float (&u)[
         if (si == 0) p01.x = l >= c ? p01.x : 0.f;  // rows above the pivot: skipped
     }
     const float p[4] = {p01.x, p01.y, p23.x, p23.y};
-    const float c2 = 2.f * wave_reduce<RedOp::Sum, FAST>(p);
-    if constexpr (FAST) {
-        const float sc = c2 * recip;
+    if constexpr (FAST) {  // recip = 2 RN(1/|u|^2) (publish_pivot)
+        const float sc = wave_reduce<RedOp::Sum, true>(p) * recip;
         const f2v vs = {sc, sc};
         const float keep0 = a[0].x;
 #pragma unroll
@@ -320,6 +320,7 @@ __device__ __forceinline__ void update_column_f32(f2v (&a)[8], const float (&u)[
         __builtin_amdgcn_sched_barrier(0);
         return;
     }
+    const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);
     f2v q[kSlots / 2];
     if (fabsf(c2) < 0x1p100f && ulen2 >= 0x1p-100f && ulen2 < 0x1p100f) {
         const f2v vb = {ulen2, ulen2}, vy = {recip, recip};
@@ -499,7 +500,9 @@ __device__ __forceinline__ void publish_pivot(const P2 (&a)[8], LDS& L, int l) {
     }
     if (l == 0) {
         L.piv[buf][0] = ulen2;
-        L.piv[buf][1] = FAST ? __builtin_amdgcn_rcpf(ulen2) : 1.f / ulen2;
+        // fast_fit: 2 RN(1/|u|^2) (the update's factor RN(RN(2 dot) / ...)
+        // then takes one multiply: doubling is exact)
+        L.piv[buf][1] = FAST ? 2.f * __builtin_amdgcn_rcpf(ulen2) : 1.f / ulen2;
         L.piv[buf][2] = ucl2;
     }
     if (l < c) {  // R column: rows above the diagonal, then the diagonal

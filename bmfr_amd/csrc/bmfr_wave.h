@@ -112,8 +112,7 @@ __device__ __forceinline__ float dpp_mov(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
 }
 template <RedOp OP>
-__device__ __forceinline__ float wave_reduce_fast(const float (&p)[4]) {
-    float s = red<OP>(red<OP>(p[0], p[1]), red<OP>(p[2], p[3]));
+__device__ __forceinline__ float wave_reduce_fast(float s) {
     s = red<OP>(s, dpp_mov<0xB1>(s));   // quad_perm [1, 0, 3, 2]
     s = red<OP>(s, dpp_mov<0x4E>(s));   // quad_perm [2, 3, 0, 1]
     s = red<OP>(s, dpp_mov<0x141>(s));  // row_half_mirror
@@ -124,6 +123,10 @@ __device__ __forceinline__ float wave_reduce_fast(const float (&p)[4]) {
     s = red<OP>(__int_as_float(sw[0]), __int_as_float(sw[1]));  // halves
     if constexpr (OP != RedOp::Sum) s = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s)));
     return s;
+}
+template <RedOp OP>
+__device__ __forceinline__ float wave_reduce_fast(const float (&p)[4]) {
+    return wave_reduce_fast<OP>(red<OP>(red<OP>(p[0], p[1]), red<OP>(p[2], p[3])));
 }
 
 // K independent sums at once, for one wave: lane l holds the step-2 values
