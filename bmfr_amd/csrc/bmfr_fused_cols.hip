@@ -843,7 +843,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 #endif
     // 0: own 8 rows; 1: slot NW i + w; 2: item pairs interleaved (slots 2 NW (i / 2) + 2 w + (i & 1):
     // a thread's two items of a pair stay adjacent slots, one 4-byte store per column)
-    constexpr int kIlv = BMFR_K1_INTERLEAVE;
+    constexpr int kIlv = F32 ? 0 : BMFR_K1_INTERLEAVE;  // f32: wave w computes row quad w (compacted matrix)
     constexpr bool kInterleave = kIlv == 1;
     auto item_slot = [&](int i) {  // row slot j: rows l + 64 j
         return kIlv == 1 ? NW * i + w : (kIlv == 2 ? 2 * NW * (i / 2) + 2 * w + (i & 1) : NI * w + i);
