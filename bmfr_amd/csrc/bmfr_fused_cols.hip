@@ -310,7 +310,7 @@ __device__ __forceinline__ void update_column_f32(f2v (&a)[8], const float (&u)[
     }
     const float p[4] = {p01.x, p01.y, p23.x, p23.y};
     if constexpr (FAST) {  // recip = 2 RN(1/|u|^2) (publish_pivot)
-        const float sc = wave_reduce<RedOp::Sum, true>(p) * recip;
+        const float sc = wave_reduce_fast<RedOp::Sum>(p) * recip;
         const f2v vs = {sc, sc};
         const float keep0 = a[0].x;
 #pragma unroll

@@ -102,27 +102,40 @@ __device__ __forceinline__ float step2(const float (&p)[4]) {
 
 // bmfr_config.fast_fit: the wave's sum / max / min of the four partials per
 // lane as a butterfly -- quad swaps, half-row and row mirrors by DPP, then the
-// 16- and 32-lane permlane swaps: 6 dependent steps instead of upstream's
-// ~20-step association (wave_tree), so NOT upstream's rounding order.  A sum
-// ends with the same bits in every lane (each level adds two per-group-equal
-// values, a + b == b + a); min / max go through readfirstlane (fmaxf(+0, -0)
-// need not commute).
+// four rows folded by row-broadcast DPP: 6 dependent steps instead of
+// upstream's ~20-step association (wave_tree), so NOT upstream's rounding
+// order; the result is lane 63's, as a scalar.
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// Rows folded into lane 63 by two row-broadcast DPP steps (rows 1, 3 take
+// lane 15 of the row before; rows 2, 3 take lane 31), read out to a scalar:
+// three fewer VALU instructions than permlane swaps, and for a sum the same
+// association, (r0 + r1) + (r2 + r3), bit for bit.  Inline asm (the compiler
+// keeps a row-masked row_bcast as a separate mov + op), each step carrying
+// the two wait states its DPP source needs after a VALU write.
+template <RedOp OP>
+__device__ __forceinline__ float fold_rows(float s) {
+    if constexpr (OP == RedOp::Sum) {
+        asm("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf" : "+v"(s));
+        asm("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf" : "+v"(s));
+    } else if constexpr (OP == RedOp::Max) {
+        asm("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf" : "+v"(s));
+        asm("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf" : "+v"(s));
+    } else {
+        asm("s_nop 1\n\tv_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf" : "+v"(s));
+        asm("s_nop 1\n\tv_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf" : "+v"(s));
+    }
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 63));
 }
 template <RedOp OP>
 __device__ __forceinline__ float wave_reduce_fast(float s) {
     s = red<OP>(s, dpp_mov<0xB1>(s));   // quad_perm [1, 0, 3, 2]
     s = red<OP>(s, dpp_mov<0x4E>(s));   // quad_perm [2, 3, 0, 1]
     s = red<OP>(s, dpp_mov<0x141>(s));  // row_half_mirror
-    s = red<OP>(s, dpp_mov<0x140>(s));  // row_mirror
-    auto sw = __builtin_amdgcn_permlane16_swap(__float_as_int(s), __float_as_int(s), false, false);
-    s = red<OP>(__int_as_float(sw[0]), __int_as_float(sw[1]));  // rows (0, 1) and (2, 3)
-    sw = __builtin_amdgcn_permlane32_swap(__float_as_int(s), __float_as_int(s), false, false);
-    s = red<OP>(__int_as_float(sw[0]), __int_as_float(sw[1]));  // halves
-    if constexpr (OP != RedOp::Sum) s = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s)));
-    return s;
+    s = red<OP>(s, dpp_mov<0x140>(s));  // row_mirror: every lane holds its row's value
+    return fold_rows<OP>(s);            // uniform: a scalar
 }
 template <RedOp OP>
 __device__ __forceinline__ float wave_reduce_fast(const float (&p)[4]) {
