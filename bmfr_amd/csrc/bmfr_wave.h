@@ -131,11 +131,26 @@ __device__ __forceinline__ float fold_rows(float s) {
 }
 template <RedOp OP>
 __device__ __forceinline__ float wave_reduce_fast(float s) {
-    s = red<OP>(s, dpp_mov<0xB1>(s));   // quad_perm [1, 0, 3, 2]
-    s = red<OP>(s, dpp_mov<0x4E>(s));   // quad_perm [2, 3, 0, 1]
-    s = red<OP>(s, dpp_mov<0x141>(s));  // row_half_mirror
-    s = red<OP>(s, dpp_mov<0x140>(s));  // row_mirror: every lane holds its row's value
-    return fold_rows<OP>(s);            // uniform: a scalar
+    if constexpr (OP == RedOp::Sum) {  // (the compiler fuses these into v_add_f32_dpp)
+        s = s + dpp_mov<0xB1>(s);   // quad_perm [1, 0, 3, 2]
+        s = s + dpp_mov<0x4E>(s);   // quad_perm [2, 3, 0, 1]
+        s = s + dpp_mov<0x141>(s);  // row_half_mirror
+        s = s + dpp_mov<0x140>(s);  // row_mirror: every lane holds its row's sum
+    } else {
+        // min / max as fused DPP ops in asm: fmaxf / fminf on a DPP-moved
+        // operand become mov 0, mov_dpp, canonicalise, op (the operands here
+        // are features, never NaN: phase 1 maps NaN to 0)
+#define BMFR_DPP_MINMAX(ctrl)                                                                          \
+    if constexpr (OP == RedOp::Max) asm("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 " ctrl " row_mask:0xf bank_mask:0xf" \
+                                        : "+v"(s));                                                    \
+    else asm("s_nop 1\n\tv_min_f32_dpp %0, %0, %0 " ctrl " row_mask:0xf bank_mask:0xf" : "+v"(s))
+        BMFR_DPP_MINMAX("quad_perm:[1,0,3,2]");
+        BMFR_DPP_MINMAX("quad_perm:[2,3,0,1]");
+        BMFR_DPP_MINMAX("row_half_mirror");
+        BMFR_DPP_MINMAX("row_mirror");
+#undef BMFR_DPP_MINMAX
+    }
+    return fold_rows<OP>(s);  // uniform: a scalar
 }
 template <RedOp OP>
 __device__ __forceinline__ float wave_reduce_fast(const float (&p)[4]) {
