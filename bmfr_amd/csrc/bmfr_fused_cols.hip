@@ -692,34 +692,60 @@ struct WaveFit {
             constexpr int k = decltype(K)::value;
             const int c = 1 + W + NW * k;
             if (owns(W, c) && c >= NS && c < NF) {
-                float hi[4], lo[4];
+                float bmax, bmin;
+                if constexpr (FASTR) {  // min / max of the packed halves (NaN-free: phase 1 maps NaN to 0)
+                    h2 mx = a[k][0], mn = a[k][0];
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    hi[m] = -INFINITY;
-                    lo[m] = INFINITY;
-#pragma unroll
-                    for (int si = 0; si < 4; ++si) {
-                        const float v = hget(a[k], m + 4 * si);
-                        hi[m] = fmaxf(v, hi[m]);
-                        lo[m] = fminf(v, lo[m]);
+                    for (int i = 1; i < 8; ++i) {
+                        mx = __builtin_elementwise_max(mx, a[k][i]);
+                        mn = __builtin_elementwise_min(mn, a[k][i]);
                     }
+                    bmax = wave_reduce_fast<RedOp::Max>(fmaxf((float)mx[0], (float)mx[1]));
+                    bmin = wave_reduce_fast<RedOp::Min>(fminf((float)mn[0], (float)mn[1]));
+                } else {
+                    float hi[4], lo[4];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        hi[m] = -INFINITY;
+                        lo[m] = INFINITY;
+#pragma unroll
+                        for (int si = 0; si < 4; ++si) {
+                            const float v = hget(a[k], m + 4 * si);
+                            hi[m] = fmaxf(v, hi[m]);
+                            lo[m] = fminf(v, lo[m]);
+                        }
+                    }
+                    bmax = wave_reduce<RedOp::Max, FAST>(hi);
+                    bmin = wave_reduce<RedOp::Min, FAST>(lo);
                 }
-                const float bmax = wave_reduce<RedOp::Max, FAST>(hi);
-                const float bmin = wave_reduce<RedOp::Min, FAST>(lo);
                 const float d = bmax - bmin;
                 const bool divide = fabsf(d) > 1.0f;  // scale(), bmfr.cl:200-205
-                const float rcp = 1.f / d;
+                // fast_fit: the hardware reciprocal, and the scaling as ONE fused
+                // multiply-add x s + o, (s, o) = (rcp, RN(-bmin rcp)) or (1, -bmin),
+                // in phase 3 as here (fast_scale)
+                const float rcp = FAST ? __builtin_amdgcn_rcpf(d) : 1.f / d;
                 if (l == 0) {
                     L.fo().mm[3 * (c - NS)] = bmin;
                     L.fo().mm[3 * (c - NS) + 1] = bmax;
                     L.fo().mm[3 * (c - NS) + 2] = rcp;
                 }
+                if constexpr (FAST) {
+                    const float fs = divide ? rcp : 1.f, fo = divide ? -bmin * rcp : -bmin;
+                    if constexpr (FASTR) {
 #pragma unroll
-                for (int j = 0; j < kSlots; ++j) {
-                    const float v = hget(a[k], j) - bmin;
-                    // fast_fit: one multiply by the rounded reciprocal (as phase 3)
-                    const float sv = FAST ? v * rcp : div_by_recip(v, d, rcp);
-                    hset(a[k], j, divide ? sv : v);
+                        for (int i = 0; i < 8; ++i)
+                            a[k][i] = __builtin_convertvector(
+                                (f2v{fma_h<0>(a[k][i], fs, fo), fma_h<1>(a[k][i], fs, fo)}), h2);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) a[k][i] = __builtin_elementwise_fma(a[k][i], f2v{fs, fs}, f2v{fo, fo});
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < kSlots; ++j) {
+                        const float v = hget(a[k], j) - bmin;
+                        hset(a[k], j, divide ? div_by_recip(v, d, rcp) : v);
+                    }
                 }
             }
         });
@@ -1031,11 +1057,13 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
 #pragma unroll
             for (int h = kPairs ? hh : 0; h < (kPairs ? hh + 1 : NPR); ++h) {
                 f2v v = {feature_value(f, nrm[2 * h], wp[2 * h]), feature_value(f, nrm[2 * h + 1], wp[2 * h + 1])};
-                if (f >= NS) {
+                if (f >= NS && FAST) {  // fast_fit: x s + o, as the fit scaled it
+                    const bool divide = fabsf(d) > 1.0f;
+                    const float fs = divide ? rcp : 1.f, fo = divide ? -bmin * rcp : -bmin;
+                    v = __builtin_elementwise_fma(v, f2v{fs, fs}, f2v{fo, fo});
+                } else if (f >= NS) {
                     v = v - f2v{bmin, bmin};
-                    if (FAST) {
-                        if (fabsf(d) > 1.0f) v = v * f2v{rcp, rcp};  // fast_fit: as the fit scaled it
-                    } else if (fabsf(d) > 1.0f) {
+                    if (fabsf(d) > 1.0f) {
                         const f2v q0 = v * f2v{rcp, rcp};
                         const f2v r = __builtin_elementwise_fma(-q0, f2v{d, d}, v);
                         v = __builtin_elementwise_fma(r, f2v{rcp, rcp}, q0);
