@@ -386,6 +386,39 @@ __device__ __forceinline__ void update_column0(P2 (&a)[8], int l, const float* _
         for (int j = 0; j < kSlots; ++j) x[j] = BMFR_ADD_NOISE(x[j], nz[j]);
     }
 #undef BMFR_ADD_NOISE
+    if constexpr (FAST) {
+        // fast_fit: u.x as a packed pairwise tree (rows 0, 1 | 2, 3 | ...; lane
+        // 0's row 0 weighted -31), the subtraction packed
+        f2v xp[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) xp[k] = f2v{x[2 * k], x[2 * k + 1]};
+        f2v t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = xp[k];
+        t[0].x = l == 0 ? x[0] * -31.f : x[0];
+#pragma unroll
+        for (int w = 4; w >= 1; w >>= 1)
+#pragma unroll
+            for (int k = 0; k < w; ++k) t[k] = t[k] + t[k + w];
+        // the quotients correctly rounded, as upstream (q0 = -31 q instead: 1080p
+        // 1.8e-5 -> 3.2e-5 from the strict build, and no faster)
+        const float c2 = 2.f * wave_reduce_fast<RedOp::Sum>(t[0].x + t[0].y);
+        constexpr float recip = 1.f / 1984.f;
+        const float q = div_by_recip(c2, 1984.f, recip), q0 = div_by_recip(-31.f * c2, 1984.f, recip);
+        const f2v vq = {q, q};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) xp[k] = xp[k] - vq;
+        xp[0].x = l == 0 ? x[0] - q0 : xp[0].x;
+        if constexpr (std::is_same_v<P2, h2>) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a[k] = __builtin_convertvector(xp[k], h2);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a[k] = xp[k];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        return;
+    }
     float p[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -397,7 +430,7 @@ __device__ __forceinline__ void update_column0(P2 (&a)[8], int l, const float* _
         }
         p[m] = s;
     }
-    const float c2 = 2.f * wave_reduce<RedOp::Sum, FAST>(p);
+    const float c2 = 2.f * wave_reduce<RedOp::Sum>(p);
     constexpr float ulen2 = 1984.f;
     const float recip = 1.f / ulen2;
     float q, q0;
