@@ -43,7 +43,11 @@ def same_bits(a: torch.Tensor, b: torch.Tensor) -> bool:
 
 def frames_of(W, H, n, **kw):
     cfg = bmfr_amd.BmfrConfig(image_width=W, image_height=H, fast_fit=1, **kw)
-    return cfg, [bmfr_amd.synth_frame_device(W, H, f) for f in range(n)]
+    frames = [bmfr_amd.synth_frame_device(W, H, f) for f in range(n)]
+    if kw.get("input_half"):  # half3 input planes (the f32 render rounded to nearest)
+        frames = [{k: (v.half() if k in ("noisy", "normals", "positions", "albedo") else v) for k, v in fr.items()}
+                  for fr in frames]
+    return cfg, frames
 
 
 def state(den, n):
@@ -75,6 +79,8 @@ def run_frames(cfg, frames, profiled=False):
                                       (256, 144, 6, {"scaled": bmfr_amd.SCALED_THIRD_ORDER}),
                                       (200, 136, 8, {"use_half_precision_in_tmp_data": 0}),
                                       (256, 144, 6, {"use_half_precision_in_tmp_data": 0,
+                                                     "scaled": bmfr_amd.SCALED_THIRD_ORDER}),
+                                      (256, 144, 6, {"use_half_precision_in_tmp_data": 0, "input_half": 1,
                                                      "scaled": bmfr_amd.SCALED_THIRD_ORDER})])
 def test_fast_fit_frame_apis_agree(W, H, n, kw, gpu):
     """One-launch frames == profiled two-launch frames == one
