@@ -46,11 +46,13 @@ around K frames (exchange included), max over ranks.
 
 Untiled per-frame runs (the N = 1 `value`): below 4096 K1 blocks (1080p) a
 frame is one launch (K1 blocks, then the frame's TAA tiles, include/bmfr.h
-bmfr_sizes.frame_launches); HIP events around every timed frame on its
-stream give that kernel's duration (`device_ms_per_frame`,
-`roofline.launch_ms`), and `kernel_ms` -- K1 and K2 timed as separate
-launches -- comes from an untimed second pass over the same frames with
-libbmfr's per-kernel events.  Larger frames (4K, 8K) are two launches, K1
+bmfr_sizes.frame_launches) and the timed frames run with nothing between
+their launches (an event between two frames costs ~5 us of GPU time at
+1080p, profiles/r06_gap_1080p.txt): two HIP events around the timed region
+give the device's frame period (`device_ms_per_frame`); an untimed pass over
+the same frames with events around each launch gives the frame kernel's
+duration (`roofline.launch_ms`, `kernel_ms.frame_one_launch`), and another
+with libbmfr's per-kernel events K1 and K2 timed as separate launches.  Larger frames (4K, 8K) are two launches, K1
 then K2; they, sequence and tiled runs record libbmfr's per-kernel events
 (on the launch stream) on every 10th timed frame.
 
@@ -163,6 +165,19 @@ def psnr(a: np.ndarray, b: np.ndarray) -> float:
     return 10 * np.log10(1.0 / mse) if mse > 0 else float("inf")
 
 
+def cpu_model() -> str:
+    """The host CPU's model string (/proc/cpuinfo), for cpu_baseline."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(cfg: bmfr_amd.BmfrConfig, frames: int, seed: int):
     """CPU oracle on the first frames+1 frames of the same sequence; frame 0
     untimed (the reference's Total also starts at frame 1, bmfr.cpp:497-502)."""
@@ -187,6 +202,8 @@ def cpu_baseline(cfg: bmfr_amd.BmfrConfig, frames: int, seed: int):
             times.append(dt)
     ms = 1e3 * float(np.mean(times))
     return {"value": round(ms, 2), "unit": "ms/frame", "cores": pyoracle.load().oracle_threads(),
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
             "kind": "port",
             "sample": f"{W}x{H} frames 1..{frames} of the same synthetic sequence (frame 0 untimed), "
                       f"oracle/bmfr_oracle.c with OpenMP"}
@@ -327,27 +344,29 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
     # unless per_frame; tiled: frame by frame around the halo exchange.
     pipelined = grid is None and not per_frame
     # Untiled per-frame: each frame is one launch (K1 blocks + the frame's TAA
-    # tiles); HIP events around every timed frame on its stream give the
-    # frame kernel's duration, and the K1 / K2 split comes from a separate
-    # untimed pass with libbmfr's per-kernel events (which time the two as
-    # separate launches).  Elsewhere the per-kernel events run inside the
-    # timed region on every PROF_STRIDE-th frame.
+    # tiles), and nothing else is enqueued between the timed frames: an event
+    # between two frames' kernels costs ~5 us of GPU time per frame at 1080p
+    # (profiles/r06_gap_1080p.txt).  Two HIP events bracket the whole timed
+    # region on its stream (`device_ms_per_frame`: the device's frame period);
+    # the frame kernel's own duration comes from an untimed pass over the same
+    # frames with events around each launch, and the K1 / K2 split from
+    # another with libbmfr's per-kernel events (which time the two as separate
+    # launches).  Elsewhere the per-kernel events run inside the timed region
+    # on every PROF_STRIDE-th frame.
     one_launch = grid is None and per_frame and cfg.sizes().frame_launches == 1
     stride = PROF_STRIDE if steps >= PROF_STRIDE else 1
-    fev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if one_launch else None
+    tev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if one_launch else None
 
     def run_range(f0, f1, timed=False):
         if pipelined:
             den.process_sequence(frames[f0:f1], cams[f0:f1], f0)
         else:
+            if tev and timed:
+                tev[0].record(compute)
             for f in range(f0, f1):
-                if fev and timed:
-                    if f == f0:
-                        fev[0].record(compute)
-                    run(f)
-                    fev[f - f0 + 1].record(compute)
-                else:
-                    run(f, mark=timed and f % stride == 0)
+                run(f, mark=timed and not one_launch and f % stride == 0)
+            if tev and timed:
+                tev[1].record(compute)
 
     if warmup:
         run_range(0, warmup)
@@ -367,11 +386,23 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    frame_kernel_ms = None
+    frame_kernel_ms = period_ms = None
     if one_launch:
-        frame_kernel_ms = float(np.mean([fev[i].elapsed_time(fev[i + 1]) for i in range(steps)]))
-        # untimed: the same frames again, K1 and K2 timed as separate launches
+        period_ms = tev[0].elapsed_time(tev[1]) / steps
+        # untimed: the same frames again with events around each frame's launch
+        # (the frame kernel's duration), then once more with K1 and K2 timed as
+        # separate launches
         prof = bmfr_amd.Denoiser(cfg, device=local)
+        fev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * steps)]
+        for f in range(nfr):
+            fr = frames[f]
+            if f >= warmup:
+                fev[2 * (f - warmup)].record(compute)
+            prof.process_frame(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"], cams[f][0], cams[f][1], f)
+            if f >= warmup:
+                fev[2 * (f - warmup) + 1].record(compute)
+        torch.cuda.synchronize()
+        frame_kernel_ms = float(np.mean([fev[2 * i].elapsed_time(fev[2 * i + 1]) for i in range(steps)]))
         for f in range(nfr):
             if f == warmup:
                 prof.set_profiling(True, capacity=steps, stride=1)
@@ -413,7 +444,7 @@ def run_sequence(a, W, H, tile, grid, rank, world, dev, backend, steps, warmup, 
         "ms_per_frame": 1e3 * elapsed / steps,
         "k1_ms": float(np.mean([p[1] for p in kprof])),
         "k2_ms": float(np.mean([p[2] for p in kprof])),
-        "dev_ms": frame_kernel_ms if one_launch else float(np.mean([p[3] for p in kprof])),
+        "dev_ms": period_ms if one_launch else float(np.mean([p[3] for p in kprof])),
         "frame_kernel_ms": frame_kernel_ms,
         "psnr": psnr(tile_of(out).cpu().numpy(), tile_of(clean).cpu().numpy()),
         "psnr_in": psnr(tile_of(noisy_tm).cpu().numpy(), tile_of(clean).cpu().numpy()),
@@ -458,9 +489,12 @@ def valu_roofline(fast_fit: bool = False):
 
 def side_line(r):
     """A secondary-size field of the N = 1 line."""
-    return {"value": round(r["ms_per_frame"], 4), "device_ms_per_frame": round(r["dev_ms"], 4),
-            "kernel_ms": {"fused_block_k1": round(r["k1_ms"], 4), "taa_k2": round(r["k2_ms"], 4)},
-            "psnr_db": round(r["psnr"], 2)}
+    d = {"value": round(r["ms_per_frame"], 4), "device_ms_per_frame": round(r["dev_ms"], 4),
+         "kernel_ms": {"fused_block_k1": round(r["k1_ms"], 4), "taa_k2": round(r["k2_ms"], 4)},
+         "psnr_db": round(r["psnr"], 2)}
+    if r["frame_kernel_ms"] is not None:  # one-launch frames: the frame kernel (untimed pass, events around it)
+        d["kernel_ms"]["frame_one_launch"] = round(r["frame_kernel_ms"], 4)
+    return d
 
 
 def variant_line(r, s: int, W: int, H: int, workload: str, kernel: str, k1_kernel: str):
@@ -628,12 +662,14 @@ def main():
             fa = fb / (r["frame_kernel_ms"] * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(fa, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(fa / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(workload + "_frame"),
-                    "kernel": ("k_fused_cols_taa<..., SAME = true>" if a.half_tmp else "k_fused_rows_taa<...>")
+                    "kernel": ("k_fused_cols_taa<..., SAME = true>" if a.half_tmp or a.fast_fit
+                               else "k_fused_rows_taa<...>")
                               + " (K1 + K2 of the frame, one launch)",
                     "algorithmic_bytes_per_launch": fb, "launch_ms": round(r["frame_kernel_ms"], 4),
-                    "launch_ms_source": "HIP events recorded around each timed frame's launch on its stream "
-                                        "(would include any idle gap between frames; the rocprofv3 kernel-trace "
-                                        "mean of the same command is in profiles/*_kernel_stats.md)",
+                    "launch_ms_source": "HIP events around each frame's launch on its stream, in an untimed "
+                                        "pass over the same frames (the timed frames run without events between "
+                                        "them); the rocprofv3 kernel-trace mean of the same command is in "
+                                        "profiles/*_kernel_stats.md",
                     "limiter": "K1 blocks: latency of phase-1 gathers and of the fit's pivot chain, VALU issue "
                                "(roofline_k1); TAA tiles: texture path / latency (roofline_k2) -- not HBM"}
         else:
@@ -706,7 +742,7 @@ def main():
             wl = f"bmfr_{W}x{H}_B{rv['cfg'].buffer_count}_{'half' if b.half_tmp else 'f32'}tmp" + \
                  ("_f16in" if b.input_half else "") + ("_fastfit" if b.fast_fit else "")
             line[f"ms_per_frame_{key}"] = variant_line(rv, vs, W, H, wl, "k_fused_cols_taa<..., SAME = true>"
-                                                       if b.half_tmp else "k_fused_rows_taa<...>",
+                                                       if b.half_tmp or b.fast_fit else "k_fused_rows_taa<...>",
                                                        "k_fused_cols" if b.half_tmp or b.fast_fit else "k_fused")
         if world == 1 and a.cpu_frames > 0:
             line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_frames, a.seed)

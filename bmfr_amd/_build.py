@@ -22,7 +22,8 @@ SOURCES = ["bmfr_kernels.hip", "bmfr_fused.hip", "bmfr_fused_cols.hip", "bmfr_fu
            "bmfr_generic_ns1.hip", "bmfr_generic_ns2.hip", "bmfr_generic_ns3.hip", "bmfr_generic_ns4.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize",
          "-Wall", "-Wno-unused-function"]
-LINK_FLAGS = ["--offload-arch=gfx950", "-shared", "-fPIC", "-ldl"]
+LINK_FLAGS = ["--offload-arch=gfx950", "-shared", "-fPIC"]
+LINK_LIBS = ["-ldl"]  # after the objects on the link line
 
 
 INCLUDE = os.path.join(HERE, "..", "include")
@@ -42,7 +43,7 @@ def source_hash() -> str:
     -fno-slp-vectorize): the build id libbmfr.so carries (bmfr_build_id())
     and the loader checks (_lib.load)."""
     h = hashlib.sha256()
-    h.update(" ".join(FLAGS).encode() + b"\0" + " ".join(LINK_FLAGS).encode() + b"\0")
+    h.update(" ".join(FLAGS).encode() + b"\0" + " ".join(LINK_FLAGS + LINK_LIBS).encode() + b"\0")
     for f in source_files():
         h.update(os.path.basename(f).encode() + b"\0")
         with open(f, "rb") as fh:
@@ -130,7 +131,7 @@ def _build(force, verbose, diag, variant, extra_flags) -> str:
     with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     tmp = lib + ".tmp"
-    subprocess.run([HIPCC, *LINK_FLAGS[:-1], "-o", tmp, *objs, LINK_FLAGS[-1]], check=True)
+    subprocess.run([HIPCC, *LINK_FLAGS, "-o", tmp, *objs, *LINK_LIBS], check=True)
     os.replace(tmp, lib)
     return lib
 

@@ -48,9 +48,14 @@ struct bmfr_ctx {
     // Every context: page-locked words the kernels set when a bounded wait
     // gave up ([kSyncPivot], [kSyncTile]: frame + 1), and an event after the
     // last enqueued frame (bmfr_frame_status / bmfr_halo_status wait on it).
+    // The event is recorded only when a wait needs it (wait_frames), on the
+    // stream of the last enqueued frame: a marker between two frames' kernels
+    // costs ~6 us of GPU time per frame (profiles/r06_gap_1080p.txt).
     volatile unsigned* sync_host = nullptr;
     hipEvent_t frame_event = nullptr;
+    hipStream_t last_stream = nullptr;
     bool frame_enqueued = false;
+    bool event_pending = false;  // frames enqueued since frame_event was last recorded
     // One-launch frames (untiled canonical half-tmp_data path): per K1 block
     // the epoch of the last launch that completed it; epoch counts launches.
     unsigned* done = nullptr;
@@ -402,9 +407,9 @@ bmfr_status bmfr_create(const bmfr_config* cfg, int device, bmfr_ctx** out) {
 bmfr_status bmfr_destroy(bmfr_ctx* c) {
     if (!c) return BMFR_ERROR_INVALID_ARGUMENT;
     DeviceGuard guard(c->device);
+    if (c->frame_enqueued) (void)hipDeviceSynchronize();  // no kernel still uses the buffers or host words
     (void)hipFree(c->reach_dev);
     (void)hipFree(c->done);
-    if (c->frame_event) (void)hipEventSynchronize(c->frame_event);  // no kernel still writes the host words
     if (c->reach_host) (void)hipHostFree(const_cast<unsigned*>(c->reach_host));
     if (c->sync_host) (void)hipHostFree(const_cast<unsigned*>(c->sync_host));
     if (c->frame_event) (void)hipEventDestroy(c->frame_event);
@@ -570,6 +575,23 @@ bmfr_status reported(const bmfr_ctx* c) {
     return BMFR_OK;
 }
 
+// Waits until every frame enqueued so far has completed: frame_event, recorded
+// now on the last frame's stream if frames were enqueued since its last record
+// (falls back to a device-wide wait if that stream no longer takes a record).
+bmfr_status wait_frames(bmfr_ctx* c) {
+    if (!c->frame_enqueued) return BMFR_OK;
+    if (c->event_pending) {
+        if (hipEventRecord(c->frame_event, c->last_stream) != hipSuccess) {
+            (void)hipGetLastError();
+            const bmfr_status st = hip_status(hipDeviceSynchronize());
+            if (st == BMFR_OK) c->event_pending = false, c->frame_enqueued = false;
+            return st;
+        }
+        c->event_pending = false;
+    }
+    return hip_status(hipEventSynchronize(c->frame_event));
+}
+
 // Before a frame is enqueued: BMFR_ERROR_SYNC_TIMEOUT once a completed frame
 // reported an exhausted wait, and (tiled contexts) BMFR_ERROR_HALO_EXCEEDED
 // once one reported reprojection taps past the exchanged state -- both sticky
@@ -578,10 +600,8 @@ bmfr_status reported(const bmfr_ctx* c) {
 // cleared), then clears them.
 bmfr_status status_check(bmfr_ctx* c, int frame_number) {
     if (frame_number == 0) {
-        if (c->frame_enqueued) {
-            const bmfr_status st = hip_status(hipEventSynchronize(c->frame_event));
-            if (st != BMFR_OK) return st;
-        }
+        const bmfr_status st = wait_frames(c);
+        if (st != BMFR_OK) return st;
         c->sync_host[0] = c->sync_host[1] = 0;
         if (c->reach_host) c->reach_host[0] = 0;
         return BMFR_OK;
@@ -589,9 +609,11 @@ bmfr_status status_check(bmfr_ctx* c, int frame_number) {
     return reported(c);
 }
 
-// After a frame's last kernel: the event bmfr_frame_status waits on.
+// After a frame's last kernel: remember its stream for wait_frames (no marker
+// on the stream: the next frame's kernel follows this one directly).
 void frame_enqueued(bmfr_ctx* c, hipStream_t s) {
-    (void)hipEventRecord(c->frame_event, s);
+    c->last_stream = s;
+    c->event_pending = true;
     c->frame_enqueued = true;
 }
 
@@ -1006,10 +1028,8 @@ bmfr_status bmfr_halo_status(bmfr_ctx* c, unsigned* overshoot) {
     if (!c) return BMFR_ERROR_INVALID_ARGUMENT;
     if (overshoot) *overshoot = 0;
     DeviceGuard guard(c->device);
-    if (c->frame_enqueued) {
-        const bmfr_status st = hip_status(hipEventSynchronize(c->frame_event));
-        if (st != BMFR_OK) return st;
-    }
+    const bmfr_status st = wait_frames(c);
+    if (st != BMFR_OK) return st;
     if (c->reach_host && overshoot) *overshoot = c->reach_host[0];  // untiled: the whole image is valid state
     return reported(c);
 }

@@ -407,14 +407,19 @@ bmfr_status bmfr_exchange_run_all(bmfr_exchange* const* xs, int n, void* const* 
     // a plan error (the RCCL receive would be truncated or wait forever).
     for (int i = 1; i < n; ++i)
         if (xs[i]->device != xs[0]->device) return BMFR_ERROR_UNSUPPORTED;
-    const hipStream_t s = reinterpret_cast<hipStream_t>(streams[0]);
-    for (int i = 0; i < n && st == BMFR_OK; ++i) st = pack(xs[i], s, f);
-    if (st != BMFR_OK) return st;
+    // Both ends of every message are matched before anything is queued (a bad
+    // plan is refused with nothing enqueued): (receiver, rbuf offset, sender,
+    // sbuf offset, bytes) per message.
+    struct Copy {
+        int to, from;
+        size_t ro, so, bytes;
+    };
+    std::vector<Copy> copies;
     for (int i = 0; i < n; ++i) {  // receiver i
-        bmfr_exchange* x = xs[i];
         size_t ro = 0;
-        for (const auto& p : x->plans[f]) {
+        for (const auto& p : xs[i]->plans[f]) {
             if (p.recv_bytes) {
+                if (p.peer < 0 || p.peer >= n) return BMFR_ERROR_INVALID_ARGUMENT;
                 const bmfr_exchange* y = xs[p.peer];  // the sender
                 size_t so = 0;
                 const PeerPlan* q = nullptr;
@@ -426,11 +431,18 @@ bmfr_status bmfr_exchange_run_all(bmfr_exchange* const* xs, int n, void* const* 
                     so += yp.send_bytes;
                 }
                 if (!q || q->send_bytes != p.recv_bytes || q->send != p.recv) return BMFR_ERROR_INVALID_ARGUMENT;
-                const hipError_t e = hipMemcpyAsync(x->rbuf + ro, y->sbuf + so, p.recv_bytes, hipMemcpyDeviceToDevice, s);
-                if (e != hipSuccess) return hip_st(e);
+                copies.push_back({i, p.peer, ro, so, p.recv_bytes});
             }
             ro += p.recv_bytes;
         }
+    }
+    const hipStream_t s = reinterpret_cast<hipStream_t>(streams[0]);
+    for (int i = 0; i < n && st == BMFR_OK; ++i) st = pack(xs[i], s, f);
+    if (st != BMFR_OK) return st;
+    for (const Copy& c : copies) {
+        const hipError_t e =
+            hipMemcpyAsync(xs[c.to]->rbuf + c.ro, xs[c.from]->sbuf + c.so, c.bytes, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return hip_st(e);
     }
     for (int i = 0; i < n && st == BMFR_OK; ++i) st = unpack(xs[i], s, f);
     return st;

@@ -1254,8 +1254,12 @@ namespace {
 #endif
 constexpr bool kColsExact = !kColsF32 || BMFR_F32_COLS_EXACT;
 
+// false (nothing launched): a configuration this translation unit has no
+// kernel for -- the f32 unit compiles only the fast fit, so a strict f32
+// context that reached it without fused_cols_supported gets an error, never
+// the non-reference fit.
 template <template <int, class, bool> class L, class... Args>
-void dispatch_cols(const Params& Q, Args&&... args) {
+bool dispatch_cols(const Params& Q, Args&&... args) {
     if constexpr (kColsExact) {
         if (Q.scaled == 6) {
             if (Q.input_half) Q.fast_fit ? L<6, _Float16, true>::go(args...) : L<6, _Float16, false>::go(args...);
@@ -1264,10 +1268,12 @@ void dispatch_cols(const Params& Q, Args&&... args) {
             if (Q.input_half) Q.fast_fit ? L<9, _Float16, true>::go(args...) : L<9, _Float16, false>::go(args...);
             else Q.fast_fit ? L<9, float, true>::go(args...) : L<9, float, false>::go(args...);
         }
-    } else {  // callers check fused_cols_supported
+    } else {
+        if (!Q.fast_fit) return false;
         if (Q.scaled == 6) Q.input_half ? L<6, _Float16, true>::go(args...) : L<6, float, true>::go(args...);
         else Q.input_half ? L<9, _Float16, true>::go(args...) : L<9, float, true>::go(args...);
     }
+    return true;
 }
 
 template <int FS, class IN, bool FAST>
@@ -1305,18 +1311,18 @@ struct LaunchColsTaa {
 
 template <>
 hipError_t launch_cols_k1<kColsF32>(const Params& P, hipStream_t st, const FusedArgs& A) {
-    dispatch_cols<LaunchCols>(P, P, st, A);
+    if (!dispatch_cols<LaunchCols>(P, P, st, A)) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 template <>
 hipError_t launch_cols_frame_one<kColsF32>(const Params& P, hipStream_t st, const FusedArgs& A) {
-    dispatch_cols<LaunchFrameOne>(P, P, st, A);
+    if (!dispatch_cols<LaunchFrameOne>(P, P, st, A)) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 template <>
 hipError_t launch_cols_k1_taa<kColsF32>(const Params& P, hipStream_t st, const FusedArgs* A, const Params& P2,
                                         const FusedArgs* A2) {
-    dispatch_cols<LaunchColsTaa>(A ? P : P2, P, st, A, P2, A2);
+    if (!dispatch_cols<LaunchColsTaa>(A ? P : P2, P, st, A, P2, A2)) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

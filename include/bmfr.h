@@ -368,7 +368,11 @@ bmfr_status bmfr_halo_status(bmfr_ctx *ctx, unsigned *overshoot);
  * else BMFR_OK.  Every bmfr_process_frame* / bmfr_process_sequence call
  * returns the same report, without waiting, once the host has seen it, until
  * frame_number 0 starts a new sequence (frame 0 first waits for every frame
- * enqueued before it, then clears the reports). */
+ * enqueued before it, then clears the reports).  The wait is an event the
+ * library records at that point on the stream of the last enqueued frame
+ * (none between frames: a marker between two frames' kernels costs GPU time),
+ * so it also waits for work the caller queued on that stream after the frame;
+ * if that stream no longer exists it waits for the whole device. */
 bmfr_status bmfr_frame_status(bmfr_ctx *ctx);
 
 /* Device pointer to the last processed frame's output (TAA result, float3,

@@ -153,3 +153,25 @@ def test_delayed_k1_blocks_tiled_border_launch_exact(gpu):
             a = got[y - ry:y - ry + h, x - rx:x - rx + w].contiguous().view(torch.int32)
             b = want[y:y + h, x:x + w].contiguous().view(torch.int32)
             assert torch.equal(a, b), (f, r, int((a != b).sum()))
+
+
+@pytest.mark.parametrize("W,H", [(1920, 1080), (3840, 2160)])
+def test_frame_status_waits_for_the_last_frames_stream(W, H, gpu):
+    """bmfr_frame_status records its event when called, on the stream of the
+    last enqueued frame (no marker between frames): after it returns, that
+    stream has drained -- here a side stream whose frames carry delayed K1
+    blocks (one in 61 sleeps ~40 us x 40), one-launch (1080p) and two-launch
+    (4K) frames alike -- and frame 0 of a new sequence waits the same way."""
+    den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=W, image_height=H))
+    frames = _frames(W, H, 3)
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    den.debug_sync(k1_delay=40)
+    with torch.cuda.stream(s):
+        _run(den, frames)
+    assert den.frame_status() == 0
+    assert s.query(), "bmfr_frame_status returned before the last frame's stream drained"
+    with torch.cuda.stream(s):
+        _run(den, frames)  # frame 0 again: waits for the frames above, clears the reports
+    assert den.frame_status() == 0
+    assert s.query()
