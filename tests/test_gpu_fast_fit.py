@@ -102,9 +102,10 @@ def test_fast_fit_frame_apis_agree(W, H, n, kw, gpu):
     assert rel_l2(one[-1]["result"], exact[-1]["result"]) < TOL
 
 
-# (reference build, frames): every block-grid offset at 1080p / 4K, B = 16, a 60-frame sequence
+# (reference build, frames): every block-grid offset at 1080p / 4K, B = 16, 60-frame sequences (720p, 4K and
+# BASELINE config 2's 1080p)
 CASES = [("f1920x1080_h13", 17), ("f3840x2160_h13", 17), ("f3840x2160_h16", 17), ("f3840x2160_f13", 17),
-         ("f1280x720_h13", 60), ("f3840x2160_h13", 60)]
+         ("f1280x720_h13", 60), ("f3840x2160_h13", 60), ("f1920x1080_h13", 60)]
 
 
 @pytest.mark.parametrize("name,n", CASES)
