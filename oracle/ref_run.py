@@ -148,7 +148,12 @@ class RefLoop:
         self.cur(self.positions)[:n].copy_(positions.reshape(-1))
         self.albedo.copy_(albedo.reshape(-1))
 
-    def run_stages(self, prev_vp, jitter, frame: int, record=None) -> None:
+    def run_stages(self, prev_vp, jitter, frame: int, record=None, upstream_launch: bool = False) -> None:
+        """One frame of tasks().  upstream_launch: accumulate_noisy_data as
+        the reference launches it (its own kernel, one launch over the margin
+        grid, bmfr.cpp:446-447) instead of the race-free margin / owner pass
+        pair -- the form the reference-speed test times; its margin values
+        may then differ by the A.4 race, so parity tests keep the default."""
         rc, m = self.rc, self.m
         ww, wh = rc.workset
         mw, mh = rc.margins
@@ -157,8 +162,11 @@ class RefLoop:
                     self.cur(self.positions), self.prev(self.positions), self.cur(self.noisy),
                     self.prev(self.noisy), self.prev(self.spp), self.cur(self.spp), self.tmp,
                     ("f", prev_vp), ("f", jitter), fr]
-        for pas in (0, 1):  # margins first, then owners (race-free semantics)
-            m.launch("ref_accumulate_noisy_data", (mw // 8, mh // 8, 1), (8, 8, 1), acc_args + [("i", pas)])
+        if upstream_launch:
+            m.launch("accumulate_noisy_data", (mw // 8, mh // 8, 1), (8, 8, 1), acc_args)
+        else:
+            for pas in (0, 1):  # margins first, then owners (race-free semantics)
+                m.launch("ref_accumulate_noisy_data", (mw // 8, mh // 8, 1), (8, 8, 1), acc_args + [("i", pas)])
         if record is not None:
             record["tmp_noisy"] = self.tmp.clone()
         m.launch("ref_fitter", (rc.blocks, 1, 1), (256, 1, 1), [self.weights, self.mins_maxs, self.tmp, fr])
