@@ -173,6 +173,15 @@ __device__ __forceinline__ In3<IN> ld3raw(const float* __restrict__ b, uint32_t 
     if constexpr (sizeof(IN) == 2) return In3<IN>{*reinterpret_cast<const h3raw*>(at_byte(b, x6(i)))};
     else return In3<IN>{ld3(b, i)};
 }
+// Two horizontally adjacent half3 pixels (i, i + 1) of a plane in one 12-byte
+// load: .x = pixel i's x | y << 16, .y = its z | pixel i + 1's x << 16, .z =
+// pixel i + 1's y | z << 16.
+struct __attribute__((packed, aligned(2))) h3pair {
+    uint32_t a, b, c;
+};
+__device__ __forceinline__ h3pair ld3pair_h(const float* __restrict__ b, uint32_t i) {
+    return *reinterpret_cast<const h3pair*>(at_byte(b, x6(i)));
+}
 __device__ __forceinline__ f3 widen(const In3<float>& r) { return r.v; }
 __device__ __forceinline__ f3 widen(const In3<_Float16>& r) {
     return f3{(float)__builtin_bit_cast(_Float16, (uint16_t)(r.v.xy & 0xffffu)),

@@ -140,6 +140,43 @@ __device__ __forceinline__ float lane_value(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
+// Phase 1 -> 3 in registers: an item's normal and position as loaded.  f32
+// inputs: six floats.  Half inputs: the 12 bytes in three registers (the two
+// .xy words and both .z halves in one), not four.
+#ifndef BMFR_KEEP_NP_HALF_IN
+#define BMFR_KEEP_NP_HALF_IN 0
+#endif
+#ifndef BMFR_KEEP_NP_F32
+#define BMFR_KEEP_NP_F32 0
+#endif
+template <class IN>
+struct KeptNP {
+    In3<IN> n, p;
+    __device__ __forceinline__ void set(const In3<IN>& nrm, const In3<IN>& wp) {
+        n = nrm;
+        p = wp;
+    }
+    __device__ __forceinline__ void get(In3<IN>& nrm, In3<IN>& wp) const {
+        nrm = n;
+        wp = p;
+    }
+};
+template <>
+struct KeptNP<_Float16> {
+    uint32_t nxy, pxy, z;  // z: n.z | p.z << 16
+    __device__ __forceinline__ void set(const In3<_Float16>& nrm, const In3<_Float16>& wp) {
+        nxy = nrm.v.xy;
+        pxy = wp.v.xy;
+        z = (uint32_t)nrm.v.z | ((uint32_t)wp.v.z << 16);
+    }
+    __device__ __forceinline__ void get(In3<_Float16>& nrm, In3<_Float16>& wp) const {
+        nrm.v.xy = nxy;
+        nrm.v.z = (uint16_t)(z & 0xffffu);
+        wp.v.xy = pxy;
+        wp.v.z = (uint16_t)(z >> 16);
+    }
+};
+
 // Sum over the wave of upstream work-item partials p[m] (work-item l + 64 m),
 // in upstream's association (bmfr.cl:25-44); with FAST (bmfr_config.fast_fit)
 // a butterfly instead (wave_reduce_fast).
@@ -928,8 +965,13 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     // phase 3 (no second read of those planes: 24 B/px of f32 input; K1
     // -4 %); the exact fit (K1 +12 %, 84-96 bytes of spills) and B = 16
     // (76-144 bytes) hold too many registers for it.
-    constexpr bool kKeepNP = FASTR && B < 16;
-    In3<IN> keep_n[NI], keep_p[NI];
+#ifdef BMFR_KEEP_NP_ALL
+    constexpr bool kKeepNP = true;
+#else
+    constexpr bool kKeepNP = FAST && (F32 ? BMFR_KEEP_NP_F32 && B < 16
+                                          : B < 16 || BMFR_KEEP_NP_HALF_IN && sizeof(IN) == 2);
+#endif
+    KeptNP<IN> keep_np[NI];
     NoisyCur<IN> cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + item_row(l, 0), frame);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -938,10 +980,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
         if (i < NI - 1) nxt = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + item_row(l, i + 1), frame);
         __builtin_amdgcn_sched_barrier(0);
         const NoisyItem it = noisy_taps_finish<true, IN>(P, cur, tp, frame);
-        if constexpr (kKeepNP) {
-            keep_n[i] = cur.nrm;
-            keep_p[i] = cur.wp;
-        }
+        if constexpr (kKeepNP) keep_np[i].set(cur.nrm, cur.wp);
         {
 #pragma unroll
             for (int f = 1; f < B; ++f) {
@@ -1027,8 +1066,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
         const int py = by * kEdge + item_row(l3, i) - kEdge / 2 + off.y;
         lin[i] = pix(P, (ibits & (1u << i)) ? px : P.ox, (ibits & (1u << i)) ? py : P.oy);  // margins: a valid pixel, skipped below
         if constexpr (kKeepNP) {
-            nrm_r[i] = keep_n[i];
-            wp_r[i] = keep_p[i];
+            keep_np[i].get(nrm_r[i], wp_r[i]);
         } else {
             nrm_r[i] = ld3raw<IN>(A.in.n_cur, lin[i]);
             wp_r[i] = ld3raw<IN>(A.in.p_cur, lin[i]);

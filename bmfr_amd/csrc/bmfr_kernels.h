@@ -293,9 +293,24 @@ __device__ __forceinline__ NoisyCur<IN> noisy_load_current(const Params& P, cons
 // current-frame loads while this item's taps are in flight: _issue does the
 // reprojection (bmfr.cl:343-372) and issues the tap loads, _finish tests,
 // weighs and blends them (bmfr.cl:374-445).
+// Half input planes: previous position / normal taps loaded a row pair at a
+// time (noisy_taps_issue); -DBMFR_PAIR_TAPS=0 loads them pixel by pixel.
+#ifndef BMFR_PAIR_TAPS
+#define BMFR_PAIR_TAPS 1
+#endif
+template <class IN>
+constexpr bool kPairTaps = BMFR_PAIR_TAPS && sizeof(IN) == 2;
+
 template <class IN = float>
 struct NoisyTaps {
     In3<IN> pp[4], pn[4];  // previous position / normal (input planes), as loaded
+    // half input planes (kPairTaps): the previous position / normal of tap row
+    // r's two pixels as one 12-byte load each, split into pp / pn in _finish;
+    // fix bit 2 r: the row's pair was read one pixel to the right (it would
+    // start before the plane), bit 2 r + 1: one to the left (it would end past it)
+    h3pair pq[2], nq[2];
+    uint32_t fix;
+    bool any_fix;  // wave-uniform: some lane has a fix bit
     f3 pc[4], pa[4];
     // spp taps as loaded (u8 zero-extended): converted in _finish, so no
     // conversion -- and no wait for the loads -- sits in the issue half
@@ -407,10 +422,36 @@ __device__ __forceinline__ NoisyTaps<IN> noisy_taps_issue(const Params& P, const
 #endif
         }
 #ifndef BMFR_PROBE_K1_NOTAPS
+        if constexpr (kPairTaps<IN>) {
+            // Half input planes: a tap row's two pixels (ix, y), (ix + 1, y) in
+            // one 12-byte load per plane instead of two loads per pixel (a
+            // dword and a short).  The pair starts at ix clamped to
+            // [ox - 1, ox + stride - 1]: in-region taps are read where they lie,
+            // an out-of-region one (ignored, or a reach overshoot the context
+            // reports) from a neighbouring row.  Only a pair starting at linear
+            // index -1 or n - 1 would leave the plane: it is read one pixel
+            // over, and _finish takes its in-region tap from the other half.
+            const int n = P.stride * P.rows;
+            const int xc = min(max(r.ix, P.ox - 1), P.ox + P.stride - 1) - P.ox;
+            uint32_t spair[2];
+            tp.fix = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) tp.pp[i] = ld3raw<IN>(in.p_prev, sidx[i]);
+            for (int row = 0; row < 2; ++row) {
+                const int sr = (int)__umul24((uint32_t)(clamp_ry(P, r.iy + row) - P.oy), (uint32_t)P.stride) + xc;
+                spair[row] = (uint32_t)min(max(sr, 0), n - 2);
+                tp.fix |= ((uint32_t)(sr < 0) << (2 * row)) | ((uint32_t)(sr > n - 2) << (2 * row + 1));
+            }
+            tp.any_fix = __builtin_amdgcn_ballot_w64(tp.fix != 0) != 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) tp.pn[i] = ld3raw<IN>(in.n_prev, sidx[i]);
+            for (int row = 0; row < 2; ++row) tp.pq[row] = ld3pair_h(in.p_prev, spair[row]);
+#pragma unroll
+            for (int row = 0; row < 2; ++row) tp.nq[row] = ld3pair_h(in.n_prev, spair[row]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tp.pp[i] = ld3raw<IN>(in.p_prev, sidx[i]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tp.pn[i] = ld3raw<IN>(in.n_prev, sidx[i]);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) tp.pc[i] = ld3(in.noisy_prev, sidx[i]);
 #pragma unroll
@@ -505,11 +546,42 @@ __device__ __forceinline__ NoisyItem taps_blend(const Params& P, const f3& cur, 
     return o;
 }
 
+// The four taps of a plane from its two row pairs (noisy_taps_issue, half
+// input planes): tap 2 r + k is pixel k of row r's pair, except where the
+// pair was read one pixel over (fix bits, see NoisyTaps): then the in-region
+// tap is the pair's other pixel.
+__device__ __forceinline__ void split_pairs(const h3pair (&q)[2], uint32_t fix, bool any_fix, In3<_Float16> (&t)[4]) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        t[2 * r].v.xy = q[r].a;
+        t[2 * r].v.z = (uint16_t)(q[r].b & 0xffffu);
+        t[2 * r + 1].v.xy = __builtin_amdgcn_alignbit(q[r].c, q[r].b, 16);
+        t[2 * r + 1].v.z = (uint16_t)(q[r].c >> 16);
+    }
+    if (any_fix) {  // wave-uniform, and only at the plane's first / last pixel
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            if (fix & (1u << (2 * r))) t[2 * r + 1] = t[2 * r];    // read from pixel 0: tap 1 is its first pixel
+            if (fix & (2u << (2 * r))) t[2 * r] = t[2 * r + 1];    // read from pixel n - 2: tap 0 is its second
+        }
+    }
+}
+
 template <bool FILT = false, class IN = float>
 __device__ __forceinline__ NoisyItem noisy_taps_finish(const Params& P, const NoisyCur<IN>& c,
                                                       const NoisyTaps<IN>& tp, int frame) {
     const f3 wp = widen(c.wp), nrm = widen(c.nrm), cur = widen(c.cur);
-    const uint32_t accept = frame > 0 ? taps_accept<IN>(P, wp, nrm, tp.pp, tp.pn, tp.inb) : 0u;
+    uint32_t accept = 0u;
+    if constexpr (kPairTaps<IN>) {
+        if (frame > 0) {
+            In3<IN> pp[4], pn[4];
+            split_pairs(tp.pq, tp.fix, tp.any_fix, pp);
+            split_pairs(tp.nq, tp.fix, tp.any_fix, pn);
+            accept = taps_accept<IN>(P, wp, nrm, pp, pn, tp.inb);
+        }
+    } else {
+        accept = frame > 0 ? taps_accept<IN>(P, wp, nrm, tp.pp, tp.pn, tp.inb) : 0u;
+    }
     NoisyItem o = taps_blend<FILT>(P, cur, accept, tp.wts, tp.pc, tp.spu, tp.pa, tp.pfx, tp.pfy, tp.over,
                                    pix(P, c.px, c.py), c.owner, frame);
     o.n = nrm;
