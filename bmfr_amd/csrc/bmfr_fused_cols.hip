@@ -969,7 +969,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     constexpr bool kKeepNP = true;
 #else
     constexpr bool kKeepNP = FAST && (F32 ? BMFR_KEEP_NP_F32 && B < 16
-                                          : B < 16 || BMFR_KEEP_NP_HALF_IN && sizeof(IN) == 2);
+                                          : B < 16 || (BMFR_KEEP_NP_HALF_IN && sizeof(IN) == 2));
 #endif
     KeptNP<IN> keep_np[NI];
     NoisyCur<IN> cur = noisy_load_current<IN>(P, A.in, bx * kEdge + lx, by * kEdge + item_row(l, 0), frame);
