@@ -148,13 +148,23 @@ class RefLoop:
         self.cur(self.positions)[:n].copy_(positions.reshape(-1))
         self.albedo.copy_(albedo.reshape(-1))
 
-    def run_stages(self, prev_vp, jitter, frame: int, record=None, upstream_launch: bool = False) -> None:
+    def run_stages(self, prev_vp, jitter, frame: int, record=None, upstream_launch: bool = False,
+                   marks=None) -> None:
         """One frame of tasks().  upstream_launch: accumulate_noisy_data as
         the reference launches it (its own kernel, one launch over the margin
         grid, bmfr.cpp:446-447) instead of the race-free margin / owner pass
         pair -- the form the reference-speed test times; its margin values
-        may then differ by the A.4 race, so parity tests keep the default."""
+        may then differ by the A.4 race, so parity tests keep the default.
+        marks: a list that receives a recorded timing event after each
+        kernel (the per-kernel split of the reference-speed test)."""
         rc, m = self.rc, self.m
+
+        def mark():
+            if marks is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                marks.append(ev)
+
         ww, wh = rc.workset
         mw, mh = rc.margins
         fr = ("i", frame)
@@ -167,18 +177,23 @@ class RefLoop:
         else:
             for pas in (0, 1):  # margins first, then owners (race-free semantics)
                 m.launch("ref_accumulate_noisy_data", (mw // 8, mh // 8, 1), (8, 8, 1), acc_args + [("i", pas)])
+        mark()
         if record is not None:
             record["tmp_noisy"] = self.tmp.clone()
         m.launch("ref_fitter", (rc.blocks, 1, 1), (256, 1, 1), [self.weights, self.mins_maxs, self.tmp, fr])
+        mark()
         g8 = (ww // 8, wh // 8, 1)
         m.launch("weighted_sum", g8, (8, 8, 1), [self.weights, self.mins_maxs, self.filtered,
                                                  self.cur(self.normals), self.cur(self.positions),
                                                  self.cur(self.noisy), fr])
+        mark()
         m.launch("accumulate_filtered_data", g8, (8, 8, 1),
                  [self.filtered, self.prev_pixels, self.accept, self.albedo, self.tone, self.cur(self.spp),
                   self.prev(self.out), self.cur(self.out), fr])
+        mark()
         m.launch("taa", g8, (8, 8, 1), [self.prev_pixels, self.tone, self.cur(self.result),
                                         self.prev(self.result), fr])
+        mark()
         if record is not None:
             W, H = rc.width, rc.height
             n = W * H

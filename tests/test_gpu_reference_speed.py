@@ -65,16 +65,22 @@ def test_reference_kernels_vs_libbmfr_same_gpu(build, nframes, warm, gpu, parity
         pytest.skip(f"reference build {build}_default missing (oracle/build_ref.py)")
     frames, cams = _frames(rc, nframes), _cams(rc, nframes)
     ref = ref_run.RefLoop(rc, "default")
+    marks = []
 
     def ref_step(f, a, b):
         fr = frames[f]
         ref.upload(fr["noisy"], fr["normals"], fr["positions"], fr["albedo"])
         a.record()
-        ref.run_stages(*cams[f], f, upstream_launch=True)
+        mk = []
+        ref.run_stages(*cams[f], f, upstream_launch=True, marks=mk)
         b.record()
+        marks.append([a] + mk)
         ref.swap()
 
     ref_ms = _time(ref_step, nframes, warm)
+    names = ("accumulate_noisy_data", "fitter", "weighted_sum", "accumulate_filtered_data", "taa")
+    ref_split = {n: sum(m[i].elapsed_time(m[i + 1]) for m in marks[warm:]) / (nframes - warm)
+                 for i, n in enumerate(names)}
     del ref
     torch.cuda.empty_cache()
     ours = {}
@@ -88,12 +94,23 @@ def test_reference_kernels_vs_libbmfr_same_gpu(build, nframes, warm, gpu, parity
             b.record()
 
         ours[name] = _time(step, nframes, warm)
+        # the K1 / K2 split: a second pass with libbmfr's per-kernel events
+        den.set_profiling(True, capacity=nframes, stride=1)
+        for f in range(nframes):
+            step(f, torch.cuda.Event(), torch.cuda.Event())
+        torch.cuda.synchronize()
+        prof = den.profile()[warm:]
+        ours[name + "_k1"] = sum(p[1] for p in prof) / len(prof)
+        ours[name + "_k2"] = sum(p[2] for p in prof) / len(prof)
         den.close()
     print(f"{build}: reference kernels {ref_ms:.4f} ms/frame; libbmfr exact {ours['exact']:.4f} "
           f"({ref_ms / ours['exact']:.2f}x), fast_fit {ours['fast_fit']:.4f} ({ref_ms / ours['fast_fit']:.2f}x)")
     parity_log(f"speed/{build}", {
         "image": f"{rc.width}x{rc.height}", "frames_averaged": nframes - warm,
         "reference_default_build_ms_per_frame": ref_ms,
+        "reference_kernels_ms": {k: round(v, 4) for k, v in ref_split.items()},
+        "libbmfr_kernels_ms": {f"{k}_{j}": round(ours[f"{k}_{j}"], 4) for k in ("exact", "fast_fit")
+                               for j in ("k1", "k2")},
         "libbmfr_exact_ms_per_frame": ours["exact"], "libbmfr_fast_fit_ms_per_frame": ours["fast_fit"],
         "speedup_exact": ref_ms / ours["exact"], "speedup_fast_fit": ref_ms / ours["fast_fit"],
         "timing": "HIP events around each frame (bmfr.cpp:495-502's START accumulate_noisy_data .. END taa)"})
