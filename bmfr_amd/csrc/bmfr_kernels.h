@@ -442,6 +442,9 @@ __device__ __forceinline__ NoisyTaps<IN> noisy_taps_issue(const Params& P, const
                 tp.fix |= ((uint32_t)(sr < 0) << (2 * row)) | ((uint32_t)(sr > n - 2) << (2 * row + 1));
             }
             tp.any_fix = __builtin_amdgcn_ballot_w64(tp.fix != 0) != 0;
+#ifdef BMFR_PROBE_NO_PAIR_FIX  // test probe (wrong results at the plane's ends): tests/test_gpu_pair_taps.py
+            tp.any_fix = false;
+#endif
 #pragma unroll
             for (int row = 0; row < 2; ++row) tp.pq[row] = ld3pair_h(in.p_prev, spair[row]);
 #pragma unroll
