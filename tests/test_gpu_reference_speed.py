@@ -8,7 +8,8 @@ REF  /root/reference/opencl/bmfr.cl compiled by oracle/build_ref.py with the
      fitter one 256-item work-group per block, weighted_sum /
      accumulate_filtered_data / taa over the workset in 8x8 work-groups.
 OURS libbmfr's bmfr_process_frame: the library default (exact fit) and the
-     bench's fast_fit.
+     bench's fast_fit, on the same feature set (B = 13, or config 5's
+     third-order B = 16; f32 input planes, as the reference reads them).
 
 Both are timed per frame the way the reference times itself (bmfr.cpp:
 495-502: START of accumulate_noisy_data to END of taa, device time, host
@@ -30,7 +31,8 @@ from ref_configs import FULL_REF_CONFIGS
 pytestmark = pytest.mark.gpu
 
 # (reference build, frames run, warm-up frames not averaged)
-CASES = [("f1920x1080_h13", 24, 4), ("f3840x2160_h13", 14, 4)]
+CASES = [("f1920x1080_h13", 24, 4), ("f3840x2160_h13", 14, 4), ("f3840x2160_h16", 14, 4),
+         ("f7680x4320_h13", 10, 3)]
 
 
 def _frames(rc, n):
@@ -85,7 +87,8 @@ def test_reference_kernels_vs_libbmfr_same_gpu(build, nframes, warm, gpu, parity
     torch.cuda.empty_cache()
     ours = {}
     for name, fast in (("exact", 0), ("fast_fit", 1)):
-        den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=rc.width, image_height=rc.height, fast_fit=fast))
+        den = bmfr_amd.Denoiser(bmfr_amd.BmfrConfig(image_width=rc.width, image_height=rc.height,
+                                                    scaled=tuple(rc.scaled), fast_fit=fast))
 
         def step(f, a, b, den=den):
             fr = frames[f]
