@@ -494,6 +494,12 @@ def side_line(r):
          "psnr_db": round(r["psnr"], 2)}
     if r["frame_kernel_ms"] is not None:  # one-launch frames: the frame kernel (untimed pass, events around it)
         d["kernel_ms"]["frame_one_launch"] = round(r["frame_kernel_ms"], 4)
+        # the frame's time outside its kernel: wall clock per frame minus the
+        # device's frame period (host issue / launch boundary), and the device
+        # period minus the kernel's own duration (idle between kernels; negative
+        # when the events around a lone kernel cost more than back-to-back launches)
+        d["gap_ms"] = {"wall_minus_device": round(r["ms_per_frame"] - r["dev_ms"], 4),
+                       "device_minus_kernel": round(r["dev_ms"] - r["frame_kernel_ms"], 4)}
     return d
 
 
