@@ -963,8 +963,10 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     float kp[NI][3];  // keep_in_m(B): the kept colours, in registers until the fit has loaded M
     // fast_fit at B = 13: phase 1's normal / position stay in registers for
     // phase 3 (no second read of those planes: 24 B/px of f32 input; K1
-    // -4 %); the exact fit (K1 +12 %, 84-96 bytes of spills) and B = 16
-    // (76-144 bytes) hold too many registers for it.
+    // -4 %).  The other K1s hold too many registers for it (round 6,
+    // profiles/r06_ab_keep_np.txt): the exact fit and f32 tmp_data spill at
+    // four work-groups per CU and lose 7-8 % at three; config 5's half inputs
+    // (three registers per item, BMFR_KEEP_NP_HALF_IN) spill 7 dwords and tie.
 #ifdef BMFR_KEEP_NP_ALL
     constexpr bool kKeepNP = true;
 #else
