@@ -521,7 +521,8 @@ def variant_line(r, s: int, W: int, H: int, workload: str, kernel: str, k1_kerne
     fa = fb / (r["frame_kernel_ms"] * 1e-3) / 1e9
     return dict(side_line(r), workload=workload,
                 roofline={"bound": "hbm", "achieved": round(fa, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": round(fa / HBM_PEAK_GBS, 4), "kernel": kernel + " (K1 + K2 of the frame, one launch)",
+                          "frac": round(fa / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(workload + "_frame"),
+                          "kernel": kernel + " (K1 + K2 of the frame, one launch)",
                           "algorithmic_bytes_per_launch": fb, "launch_ms": round(r["frame_kernel_ms"], 4)})
 
 
@@ -728,8 +729,12 @@ def main():
                      "algorithmic_bytes_per_launch": k2_bytes_per_px(s) * tile_px}, workload + "_k2", r["k2_ms"])
         if rseq is not None:
             line["ms_per_frame_sequence"] = side_line(rseq)
-        if r1080 is not None:
-            line["ms_per_frame_1080p"] = side_line(r1080)
+        if r1080 is not None:  # the metric's 1080p half: its frame kernel's roofline too
+            wl1080 = workload.replace(f"bmfr_{W}x{H}_", "bmfr_1920x1080_", 1)
+            line["ms_per_frame_1080p"] = variant_line(r1080, s, 1920, 1080, wl1080,
+                                                      "k_fused_cols_taa<..., SAME = true>" if a.half_tmp or a.fast_fit
+                                                      else "k_fused_rows_taa<...>",
+                                                      "k_fused_cols" if a.half_tmp or a.fast_fit else "k_fused")
         if r8k is not None:
             line["ms_per_frame_8k"] = dict(side_line(r8k), frames_timed=r8k["steps"])
         if r1 is not None:
