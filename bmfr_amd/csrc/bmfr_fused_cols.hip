@@ -613,9 +613,14 @@ struct WaveFit {
     static constexpr int owner(int c) { return (c - 1) % NW; }
     static constexpr int slot(int c) { return (c - 1) / NW; }
     // Step-0 noise columns prefetched per wave (slots whose column is a
-    // feature column for every wave): none at B = 16 with four waves, where
-    // the fit's registers are the limit for four work-groups per CU.
-    static constexpr int NP = B >= 16 && NW == 4 ? 0 : ((NF - 1) / NW < kPre ? (NF - 1) / NW : kPre);
+    // feature column for every wave), loaded in phase 1.  B = 16 with four
+    // waves: two as well since round 6 (its K1 now has the registers: 108
+    // VGPRs with them, no spills; config 5's K1 -1.7 to -2.2 %,
+    // profiles/r06_ab_np16.txt); -DBMFR_NP16=0 gives none.
+#ifndef BMFR_NP16
+#define BMFR_NP16 2
+#endif
+    static constexpr int NP = B >= 16 && NW == 4 ? BMFR_NP16 : ((NF - 1) / NW < kPre ? (NF - 1) / NW : kPre);
     static_assert(!F32 || NW == 4, "f32 tmp_data: row quad w of wave w");
     static_assert(NP == 0 || NW * NP < NF, "prefetched slots hold feature columns");
 
