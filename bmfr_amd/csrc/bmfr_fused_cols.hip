@@ -1108,15 +1108,20 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     for (int h = 0; h < NPR; ++h)
         for (int ch = 0; ch < 3; ++ch) cp[h][ch] = f2v{0.f, 0.f};
     // Item pairs outer where it saves registers: one pair's positions, powers
-    // and sums live at a time (features outer kept every item's in registers:
-    // 10 VGPRs of spills in the K1-only kernel at B = 13, 36-67 at B = 16
-    // with four work-groups per CU; pairs outer: none).  Features outer for
-    // the one-launch frame at B = 13, which has no spills either way and
-    // runs ~1 % faster so (each weight and min / max loaded once).
+    // and sums live at a time (features outer keeps every item's in
+    // registers: 14-67 dwords of spills at B = 16 with four work-groups per
+    // CU; pairs outer: none).  Features outer (each weight and min / max
+    // loaded once) at B = 13, where the K1s have the registers for it since
+    // round 6 (no spills; K1 -0.3 / -0.5 / -1.3 % headline / exact / f32
+    // tmp_data, profiles/r06_ab_np16.txt); -DBMFR_PAIRS_B13=1 keeps pairs
+    // outer there too.
+#ifndef BMFR_PAIRS_B13
+#define BMFR_PAIRS_B13 0
+#endif
 #ifdef PAIRS_ALL
     constexpr bool kPairs = true;
 #else
-    constexpr bool kPairs = B >= 16 || !COH || NPR == 1;
+    constexpr bool kPairs = B >= 16 || (!COH && BMFR_PAIRS_B13) || NPR == 1;
 #endif
     constexpr int NH = kPairs ? NPR : 1;
 #pragma unroll
