@@ -433,7 +433,15 @@ __device__ __forceinline__ void taa_tile(const Params& P, const TaaArgs& T, int 
 // context's last work-group then forwards the reach report once every K1
 // block of the launch has raised it.
 template <int NT>
-constexpr int frame_taa_h() { return NT == 256 ? 12 : 24; }  // 3 output rows per thread
+// Tile height of the one-launch frame's TAA tiles at 256 threads: 16 (four
+// output rows per thread; no spills beside K1's registers) against 12: 1080p
+// frame -1.2 % (fast_fit), -2.1 % (config 5), -0.4 % (exact); 8: +5 %; 20: 1
+// dword of spills, -0.8 %; 24: spills (round 6, profiles/r06_ab_frame_taa_h.txt).
+// The standalone K2 keeps 64 x 12 (BMFR_K2_H): its occupancy is its own.
+#ifndef BMFR_FRAME_TAA_H
+#define BMFR_FRAME_TAA_H 16
+#endif
+constexpr int frame_taa_h() { return NT == 256 ? BMFR_FRAME_TAA_H : 24; }  // TH / 4 output rows per thread
 template <int NT>
 struct FrameTaaLds {
     float4 Y[(64 + 2) * (frame_taa_h<NT>() + 2)];
