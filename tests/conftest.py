@@ -12,6 +12,16 @@ for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line("markers", "multi_gpu: needs two or more GPUs (RCCL between devices)")
+
+
+def pytest_collection_modifyitems(config, items):
+    # Two-GPU tests (the RCCL transport, not yet run on hardware: every box
+    # this build ran on had one GPU) go last, so that under -x a failure
+    # there cannot stop the one-GPU parity suite before it has run.
+    multi = [it for it in items if it.get_closest_marker("multi_gpu")]
+    if multi:
+        items[:] = [it for it in items if not it.get_closest_marker("multi_gpu")] + multi
 
 
 @pytest.fixture(scope="session")

@@ -137,6 +137,8 @@ def _multi_gpu_run(W, H, tx, ty, halo, frames, fast_fit):
         assert lib.bmfr_comm_destroy(comms[r]) == 0
 
 
+@pytest.mark.multi_gpu
+@pytest.mark.timeout(240, method="thread")  # a stuck RCCL call ends the run instead of hanging it
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL between ranks needs two GPUs")
 @pytest.mark.parametrize("fast_fit", [0, 1])
 def test_rccl_two_gpus_matches_untiled(fast_fit, gpu):
