@@ -859,7 +859,12 @@ template <int N>
 __device__ __forceinline__ float row_bcast(float v) {  // every lane <- lane N of its row
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + N, 0xf, 0xf, false));
 }
-template <int B, class LDS>
+// FAST (fast_fit): the division by the diagonal as a multiply by the
+// hardware reciprocal (1 ulp), which shortens the step chain's latency.
+#ifndef BMFR_FAST_BACKSUB
+#define BMFR_FAST_BACKSUB 1
+#endif
+template <int B, bool FAST, class LDS>
 __device__ __forceinline__ void back_substitute_regs(LDS& L, int t) {
     constexpr int RE = B - 2;
     static_assert(RE <= 16, "one DPP row per channel");
@@ -872,7 +877,12 @@ __device__ __forceinline__ void back_substitute_regs(LDS& L, int t) {
     sfor<RE - 1>([&](auto I) {
         constexpr int i = RE - 2 - decltype(I)::value;
         const float div = row_bcast<i>(col[i]);
-        if (live && x >= i) col[i] = col[i] / div;
+        if constexpr (FAST && BMFR_FAST_BACKSUB) {
+            const float r = __builtin_amdgcn_rcpf(div);
+            if (live && x >= i) col[i] = col[i] * r;
+        } else {
+            if (live && x >= i) col[i] = col[i] / div;
+        }
         const float v = col[i];
         // x_i = ((rhs - v[i+1]) - v[i+2]) ... - v[RE-2], rhs = v[RE-1]: the
         // running value walks from lane i+1 to lane RE-2 (src).
@@ -1081,7 +1091,7 @@ __device__ __forceinline__ void k1_cols_body(const Params& P, const K1Args& A, L
     }
     k1_barrier();  // R complete (LDS); with LDS-only barriers the loads above stay in flight
     BMFR_STAMP(3);
-    back_substitute_regs<B>(L, t);
+    back_substitute_regs<B, FAST>(L, t);
     k1_barrier();  // weights complete
     // An exhausted pivot wait: reported here, or (one-launch frame) carried by
     // the block's completion flag to the tiles that read it (fewer values
